@@ -1,0 +1,58 @@
+# Native build of veles.simd_amd: one shared library (C API + HIP kernels for
+# gfx950) and the native C API test binary.  Driven by
+# `python -m veles.simd_amd.build` / __graft_entry__.build(); plain `make -j`
+# works too.
+#
+# Copyright 2026 veles.simd_amd authors. Apache-2.0.
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+BUILD    ?= build
+LIBDIR   := veles/simd_amd/_native
+LIB      := $(LIBDIR)/libvelessimd.so
+OPT      ?= -O3
+
+COMMON   := $(OPT) -std=c++17 -fPIC -I. -Iinclude -Wall -Wextra \
+            -Wno-unused-parameter -Wno-unused-command-line-argument \
+            -DVELES_SIMD_IMPLEMENTATION -fvisibility=hidden
+HIPFLAGS := $(COMMON) -x hip --offload-arch=$(ARCH) \
+            -ffp-contract=fast
+CXXFLAGS := $(COMMON) -ffp-contract=off
+
+HIP_SRCS := $(sort $(wildcard csrc/kernels/*.hip))
+CPP_SRCS := $(sort $(wildcard csrc/runtime/*.cpp csrc/ref/*.cpp \
+              csrc/api/*.cpp csrc/data/*.cpp csrc/dist/*.cpp))
+HIP_OBJS := $(patsubst %.hip,$(BUILD)/%.o,$(HIP_SRCS))
+CPP_OBJS := $(patsubst %.cpp,$(BUILD)/%.o,$(CPP_SRCS))
+HEADERS  := $(wildcard include/simd/*.h csrc/*/*.h)
+
+TEST_BIN := $(BUILD)/tests/capi_test
+
+.PHONY: all lib tests clean
+
+all: lib tests
+
+lib: $(LIB)
+
+$(LIB): $(HIP_OBJS) $(CPP_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -Wl,-soname,libvelessimd.so \
+	    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+$(BUILD)/%.o: %.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: %.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+tests: $(TEST_BIN)
+
+$(TEST_BIN): tests/native/capi_test.cpp $(LIB) $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -O2 -std=c++17 -Iinclude -Itests/native $< -o $@ \
+	    -L$(LIBDIR) -lvelessimd -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+clean:
+	rm -rf $(BUILD) $(LIB)

@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Headline benchmark (driver contract, see README "Benchmark").
+
+Metric (BASELINE.json): "GFLOP/s SGEMM 4096^2 fp32; Msamples/s 1D conv
+len=2^20, at 1/2/4/8 MI355X".  One step = one 4096x4096x4096 exact-fp32
+SGEMM (C = A @ B, MFMA f32 kernel) per GPU; `value` is the whole-job
+aggregate GFLOP/s (weak scaling: every rank multiplies its own pair of
+matrices).  The second half of the metric, 1D convolution throughput at
+signal length 2^20 (filter 4096, batch 64 per GPU, auto-selected algorithm),
+is timed the same way and reported in `secondary`.
+
+Run: python bench.py --gpus N --steps K --warmup W   (N > 1 under
+torch.distributed.run; one rank per GPU, RCCL backend).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from veles.simd_amd import _lib  # noqa: E402
+
+SGEMM_N = 4096
+CONV_LEN = 1 << 20
+CONV_H = 4096
+CONV_BATCH = 64
+
+
+def _baseline():
+    """Reference numbers this run is divided by (None if none)."""
+    path = os.path.join(REPO, "profiles", "reference_cpu_baseline.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return {}
+
+
+def _sync_all(dist_on):
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+
+def _timed(fn, steps, warmup, dist_on):
+    for _ in range(warmup):
+        fn()
+    _sync_all(dist_on)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    _sync_all(dist_on)
+    dt = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = t.item()
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-conv", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist_on = world > 1
+    torch.cuda.set_device(local)
+    if dist_on:
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    lib = _lib.lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    # ---------------------------------------------------------------- SGEMM
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    n = SGEMM_N
+    a = torch.rand((n, n), device="cuda", generator=g) * 2 - 1
+    b = torch.rand((n, n), device="cuda", generator=g) * 2 - 1
+    c = torch.empty((n, n), device="cuda")
+    pa, pb, pc = (ctypes.c_void_p(t.data_ptr()) for t in (a, b, c))
+
+    def sgemm_step():
+        st = lib.vs_sgemm(0, 0, n, n, n, 1.0, pa, n, pb, n, 0.0, pc, n, stream)
+        if st:
+            raise RuntimeError(lib.vs_last_error().decode())
+
+    dt = _timed(sgemm_step, args.steps, args.warmup, dist_on)
+    flops = 2.0 * n * n * n * args.steps * world
+    gflops = flops / dt / 1e9
+    ms = dt / args.steps * 1e3
+
+    # Numerics guard: the timed kernel must be right.
+    ref = torch.matmul(a[:256].double(), b.double())
+    err = (c[:256].double() - ref).abs().max().item()
+    if err > 2e-6 * n:
+        raise RuntimeError(f"SGEMM numerics check failed: max err {err}")
+
+    # hipBLASLt fp32 (torch.matmul, TF32 disabled) on the same data, for context.
+    torch.backends.cuda.matmul.allow_tf32 = False
+    dt_t = _timed(lambda: torch.matmul(a, b, out=c), max(5, args.steps // 2),
+                  3, dist_on)
+    torch_gflops = 2.0 * n ** 3 * max(5, args.steps // 2) * world / dt_t / 1e9
+
+    secondary = {"torch_matmul_fp32_gflops": round(torch_gflops, 1),
+                 "sgemm_max_abs_err": err}
+
+    # ----------------------------------------------------------------- conv
+    if not args.no_conv and hasattr(lib, "vs_conv1d"):
+        x = torch.randn((CONV_BATCH, CONV_LEN), device="cuda", generator=g)
+        h = torch.randn((CONV_H,), device="cuda", generator=g)
+        ylen = CONV_LEN + CONV_H - 1
+        y = torch.empty((CONV_BATCH, ylen), device="cuda")
+        px, ph, py = (ctypes.c_void_p(t.data_ptr()) for t in (x, h, y))
+        algo = lib.vs_conv1d_select(CONV_LEN, CONV_H, CONV_BATCH)
+
+        def conv_step():
+            st = lib.vs_conv1d(0, 0, px, CONV_LEN, CONV_LEN, ph, CONV_H, 0, py,
+                               ylen, CONV_BATCH, stream)
+            if st:
+                raise RuntimeError(lib.vs_last_error().decode())
+
+        csteps = max(5, args.steps // 2)
+        dtc = _timed(conv_step, csteps, max(2, args.warmup // 2), dist_on)
+        msamples = CONV_LEN * CONV_BATCH * csteps * world / dtc / 1e6
+        secondary.update({
+            "conv1d_msamples_per_s": round(msamples, 1),
+            "conv1d_ms_per_step": round(dtc / csteps * 1e3, 3),
+            "conv1d_config": {"x_len": CONV_LEN, "h_len": CONV_H,
+                              "batch_per_gpu": CONV_BATCH,
+                              "algorithm": ["direct", "fft", "overlap_save"][
+                                  max(0, algo - 1)]},
+        })
+
+    base = _baseline()
+    vs_base = None
+    if base.get("sgemm_4096_gflops"):
+        vs_base = round(gflops / base["sgemm_4096_gflops"], 2)
+        secondary["baseline_source"] = base.get("source")
+
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GFLOP/s SGEMM 4096^2 fp32",
+            "value": round(gflops, 1),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": vs_base,
+            "dtype": "fp32",
+            "data": "synthetic (uniform [-1,1) fp32 matrices; gaussian signals)",
+            "config": {"model": "sgemm_4096x4096x4096_fp32",
+                       "global_batch": world, "seq_len": n,
+                       "parallelism": f"dp{world}"},
+            "secondary": secondary,
+        }), flush=True)
+    if dist_on:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,61 @@
+// Where does a host-API call run?  Shared policy of the source-compatible C
+// API (the reference decides at compile time with #ifdef __AVX__ and at run
+// time with the `int simd` flag, reference src/matrix.c:262-273).
+//   * simd-flag functions: simd != 0 -> GPU (if one is present), 0 -> host
+//     reference.  With no GPU the accelerated path degrades to the host
+//     reference, as the reference does on a host without SIMD.
+//   * flag-less array functions (arithmetic.h): GPU when an operand already
+//     lives in device memory or the array has >= VELES_GPU_MIN_ELEMS elements.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <initializer_list>
+
+#include "csrc/runtime/runtime.h"
+
+namespace vs {
+namespace api {
+
+inline bool any_device(std::initializer_list<const void *> ptrs) {
+  for (const void *p : ptrs)
+    if (is_device_pointer(p)) return true;
+  return false;
+}
+
+inline bool use_gpu_simd(int simd, const char *fn) {
+  if (!simd) return false;
+  if (gpu_available()) return true;
+  static bool warned = false;
+  if (!warned) {
+    warned = true;
+    log(1, "%s: no GPU visible, accelerated path runs the host reference", fn);
+  }
+  return false;
+}
+
+inline bool use_gpu_array(size_t n, std::initializer_list<const void *> ptrs) {
+  if (!gpu_available()) return false;
+  return n >= gpu_min_elems() || any_device(ptrs);
+}
+
+// Runs body(stream) on the library stream and waits for it; aborts with the
+// library error message on failure (the host API has assert() semantics).
+template <class F>
+void run_sync(const char *what, F &&body) {
+  hipStream_t s = library_stream();
+  vs_status st = body(s);
+  if (st == VS_OK) {
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      set_error("hipStreamSynchronize: %s", hipGetErrorString(e));
+      st = VS_ERR_HIP;
+    }
+  }
+  if (st != VS_OK) fatal("%s: %s", what, last_error());
+  log(2, "%s: done on GPU", what);
+}
+
+}  // namespace api
+}  // namespace vs

@@ -1,0 +1,55 @@
+// Device-side helpers shared by the CDNA4 kernels.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace vs {
+namespace dev {
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+template <class T, int N>
+struct alignas(sizeof(T) * N) Vec {
+  T v[N];
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+__device__ __forceinline__ int wave_isum(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1D block id (8 XCDs, round-robin dispatch):
+// consecutive logical tiles land on the same XCD so they share its L2
+// (cdna_hip_programming.md §5.5 T1).  Speed only, never correctness.
+__device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned nblocks) {
+  constexpr unsigned kXcd = 8;
+  if (nblocks < kXcd) return bid;
+  const unsigned q = nblocks / kXcd, r = nblocks % kXcd;
+  const unsigned xcd = bid % kXcd, pos = bid / kXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+}  // namespace dev
+}  // namespace vs

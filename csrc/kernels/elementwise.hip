@@ -1,0 +1,413 @@
+// Elementwise CDNA4 kernels: dtype conversions, real/complex arithmetic,
+// fills, reversed copies and transcendental math (SURVEY.md §2.3 K1-K4, K7,
+// K16).  These are HBM-bound; every kernel moves 4 elements per lane per
+// iteration with one vector load/store per operand (16 B for fp32) when the
+// pointers allow it, grid-strides over a grid capped at 2048 blocks, and
+// falls back to a scalar body for unaligned operands.
+//
+// Reference counterparts: inc/simd/arithmetic.h:43-191 (scalar semantics),
+// :211-830 (AVX bodies), src/memory.c:93-183, src/matrix.c:170-198,
+// inc/simd/mathfun.h:105-140.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "csrc/kernels/device.h"
+#include "csrc/runtime/runtime.h"
+#include "simd/gpu.h"
+
+namespace vs {
+namespace {
+
+using dev::Vec;
+constexpr unsigned kBlock = 256;
+
+inline bool aligned_to(const void *p, size_t a) {
+  return (reinterpret_cast<uintptr_t>(p) % a) == 0;
+}
+
+// ------------------------------------------------------------ conversions
+template <class In, class Out>
+struct Convert;
+
+template <>
+struct Convert<int16_t, float> {
+  __device__ float operator()(int16_t v) const { return static_cast<float>(v); }
+};
+template <>
+struct Convert<int32_t, float> {
+  __device__ float operator()(int32_t v) const { return static_cast<float>(v); }
+};
+template <>
+struct Convert<float, int32_t> {
+  // v_cvt_i32_f32: truncation toward zero, saturating, NaN -> 0.
+  __device__ int32_t operator()(float v) const { return __float2int_rz(v); }
+};
+template <>
+struct Convert<float, int16_t> {
+  __device__ int16_t operator()(float v) const {
+    int32_t t = __float2int_rz(v);
+    t = t < -32768 ? -32768 : (t > 32767 ? 32767 : t);
+    return static_cast<int16_t>(t);
+  }
+};
+template <>
+struct Convert<int32_t, int16_t> {
+  __device__ int16_t operator()(int32_t v) const {
+    v = v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
+    return static_cast<int16_t>(v);
+  }
+};
+template <>
+struct Convert<int16_t, int32_t> {
+  __device__ int32_t operator()(int16_t v) const { return v; }
+};
+template <>
+struct Convert<uint16_t, float> {
+  // v_cvt_f32_f16: exact for normals, subnormals, +-inf and NaN.
+  __device__ float operator()(uint16_t v) const {
+    return static_cast<float>(__builtin_bit_cast(_Float16, v));
+  }
+};
+template <>
+struct Convert<uint8_t, float> {
+  __device__ float operator()(uint8_t v) const { return static_cast<float>(v); }
+};
+template <>
+struct Convert<float, float> {
+  __device__ float operator()(float v) const { return v; }
+};
+
+template <class In, class Out, class F, int V>
+__global__ __launch_bounds__(kBlock) void map1_kernel(
+    const In *__restrict__ in, Out *__restrict__ out, size_t n, F f) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const size_t nv = n / V;
+  for (size_t i = tid; i < nv; i += stride) {
+    Vec<In, V> a = reinterpret_cast<const Vec<In, V> *>(in)[i];
+    Vec<Out, V> r;
+#pragma unroll
+    for (int j = 0; j < V; j++) r.v[j] = f(a.v[j]);
+    reinterpret_cast<Vec<Out, V> *>(out)[i] = r;
+  }
+  for (size_t i = nv * V + tid; i < n; i += stride) out[i] = f(in[i]);
+}
+
+template <class In, class Out, class F>
+vs_status launch_map1(const In *in, Out *out, size_t n, F f,
+                      hipStream_t stream) {
+  if (n == 0) return VS_OK;
+  constexpr int V = 4;
+  const bool vec = aligned_to(in, sizeof(In) * V) && aligned_to(out, sizeof(Out) * V);
+  const unsigned grid = elementwise_grid(vec ? (n + V - 1) / V : n, kBlock);
+  if (vec)
+    hipLaunchKernelGGL((map1_kernel<In, Out, F, V>), dim3(grid), dim3(kBlock),
+                       0, stream, in, out, n, f);
+  else
+    hipLaunchKernelGGL((map1_kernel<In, Out, F, 1>), dim3(grid), dim3(kBlock),
+                       0, stream, in, out, n, f);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+template <class A, class B, class Out, class F, int V>
+__global__ __launch_bounds__(kBlock) void map2_kernel(
+    const A *__restrict__ a, const B *__restrict__ b, Out *__restrict__ out,
+    size_t n, F f) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const size_t nv = n / V;
+  for (size_t i = tid; i < nv; i += stride) {
+    Vec<A, V> x = reinterpret_cast<const Vec<A, V> *>(a)[i];
+    Vec<B, V> y = reinterpret_cast<const Vec<B, V> *>(b)[i];
+    Vec<Out, V> r;
+#pragma unroll
+    for (int j = 0; j < V; j++) r.v[j] = f(x.v[j], y.v[j]);
+    reinterpret_cast<Vec<Out, V> *>(out)[i] = r;
+  }
+  for (size_t i = nv * V + tid; i < n; i += stride) out[i] = f(a[i], b[i]);
+}
+
+template <class A, class B, class Out, class F>
+vs_status launch_map2(const A *a, const B *b, Out *out, size_t n, F f,
+                      hipStream_t stream) {
+  if (n == 0) return VS_OK;
+  constexpr int V = 4;
+  const bool vec = aligned_to(a, sizeof(A) * V) && aligned_to(b, sizeof(B) * V) &&
+                   aligned_to(out, sizeof(Out) * V);
+  const unsigned grid = elementwise_grid(vec ? (n + V - 1) / V : n, kBlock);
+  if (vec)
+    hipLaunchKernelGGL((map2_kernel<A, B, Out, F, V>), dim3(grid), dim3(kBlock),
+                       0, stream, a, b, out, n, f);
+  else
+    hipLaunchKernelGGL((map2_kernel<A, B, Out, F, 1>), dim3(grid), dim3(kBlock),
+                       0, stream, a, b, out, n, f);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+struct AddOp {
+  __device__ float operator()(float x, float y) const { return x + y; }
+};
+struct SubOp {
+  __device__ float operator()(float x, float y) const { return x - y; }
+};
+struct MulOp {
+  __device__ float operator()(float x, float y) const { return x * y; }
+};
+struct Int16MulOp {
+  __device__ int32_t operator()(int16_t x, int16_t y) const {
+    return static_cast<int32_t>(x) * static_cast<int32_t>(y);
+  }
+};
+struct AffineOp {
+  float scale, shift;
+  __device__ float operator()(float x) const { return x * scale + shift; }
+};
+struct ScaleOp {
+  float scale;
+  __device__ float operator()(float x) const { return x * scale; }
+};
+struct ShiftOp {
+  float shift;
+  __device__ float operator()(float x) const { return x + shift; }
+};
+struct SaxpyOp {
+  float a;
+  __device__ float operator()(float x, float y) const { return fmaf(a, x, y); }
+};
+
+template <int FN>
+struct MathOp {
+  __device__ float operator()(float x) const {
+    if constexpr (FN == VS_FN_SIN) return sinf(x);
+    if constexpr (FN == VS_FN_COS) return cosf(x);
+    if constexpr (FN == VS_FN_LOG) return logf(x);
+    return expf(x);
+  }
+};
+
+// ------------------------------------------------------- complex kernels
+// Two interleaved complex numbers per lane (one float4).
+template <bool CONJ, int V>
+__global__ __launch_bounds__(kBlock) void cmul_kernel(
+    const float2 *__restrict__ a, const float2 *__restrict__ b,
+    float2 *__restrict__ out, size_t n) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const size_t nv = n / V;
+  for (size_t i = tid; i < nv; i += stride) {
+    Vec<float2, V> x = reinterpret_cast<const Vec<float2, V> *>(a)[i];
+    Vec<float2, V> y = reinterpret_cast<const Vec<float2, V> *>(b)[i];
+    Vec<float2, V> r;
+#pragma unroll
+    for (int j = 0; j < V; j++) {
+      const float yi = CONJ ? -y.v[j].y : y.v[j].y;
+      r.v[j].x = x.v[j].x * y.v[j].x - x.v[j].y * yi;
+      r.v[j].y = x.v[j].x * yi + y.v[j].x * x.v[j].y;
+    }
+    reinterpret_cast<Vec<float2, V> *>(out)[i] = r;
+  }
+  for (size_t i = nv * V + tid; i < n; i += stride) {
+    const float yi = CONJ ? -b[i].y : b[i].y;
+    float2 r;
+    r.x = a[i].x * b[i].x - a[i].y * yi;
+    r.y = a[i].x * yi + b[i].x * a[i].y;
+    out[i] = r;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void conj_kernel(const float *__restrict__ a,
+                                                      float *__restrict__ out,
+                                                      size_t n) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = tid; i < n; i += stride) out[i] = (i & 1) ? -a[i] : a[i];
+}
+
+__global__ __launch_bounds__(kBlock) void fill_kernel(float *__restrict__ p,
+                                                      float v, size_t n) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const bool vec = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  size_t done = 0;
+  if (vec) {
+    const size_t n4 = n / 4;
+    const float4 f = make_float4(v, v, v, v);
+    for (size_t i = tid; i < n4; i += stride) reinterpret_cast<float4 *>(p)[i] = f;
+    done = n4 * 4;
+  }
+  for (size_t i = done + tid; i < n; i += stride) p[i] = v;
+}
+
+template <bool PAIRS>
+__global__ __launch_bounds__(kBlock) void reverse_kernel(
+    const float *__restrict__ src, float *__restrict__ dst, size_t n) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  if (PAIRS) {
+    const size_t np = n / 2;
+    const float2 *s = reinterpret_cast<const float2 *>(src);
+    float2 *d = reinterpret_cast<float2 *>(dst);
+    for (size_t i = tid; i < np; i += stride) d[i] = s[np - 1 - i];
+  } else {
+    for (size_t i = tid; i < n; i += stride) dst[i] = src[n - 1 - i];
+  }
+}
+
+}  // namespace
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" {
+
+vs_status vs_convert(const void *src, int st, void *dst, int dt, size_t n,
+                     vs_stream_t stream) {
+  auto s = static_cast<hipStream_t>(stream);
+  VS_REQUIRE(src && dst, "vs_convert: null pointer");
+#define VS_CONV(ST, SD, DT, DD)                                               \
+  if (st == SD && dt == DD)                                                   \
+    return launch_map1(static_cast<const ST *>(src), static_cast<DT *>(dst), \
+                       n, Convert<ST, DT>{}, s);
+  VS_CONV(int16_t, VS_I16, float, VS_F32)
+  VS_CONV(int32_t, VS_I32, float, VS_F32)
+  VS_CONV(float, VS_F32, int32_t, VS_I32)
+  VS_CONV(float, VS_F32, int16_t, VS_I16)
+  VS_CONV(int32_t, VS_I32, int16_t, VS_I16)
+  VS_CONV(int16_t, VS_I16, int32_t, VS_I32)
+  VS_CONV(uint16_t, VS_F16, float, VS_F32)
+  VS_CONV(uint8_t, VS_U8, float, VS_F32)
+  VS_CONV(float, VS_F32, float, VS_F32)
+#undef VS_CONV
+  set_error("vs_convert: unsupported conversion %d -> %d", st, dt);
+  return VS_ERR_UNSUPPORTED;
+}
+
+vs_status vs_binary(int op, const float *a, const float *b, float *out,
+                    size_t n, vs_stream_t stream) {
+  auto s = static_cast<hipStream_t>(stream);
+  VS_REQUIRE(a && b && out, "vs_binary: null pointer");
+  switch (op) {
+    case VS_OP_ADD:
+      return launch_map2(a, b, out, n, AddOp{}, s);
+    case VS_OP_SUB:
+      return launch_map2(a, b, out, n, SubOp{}, s);
+    case VS_OP_MUL:
+      return launch_map2(a, b, out, n, MulOp{}, s);
+  }
+  set_error("vs_binary: unknown op %d", op);
+  return VS_ERR_INVALID;
+}
+
+vs_status vs_complex_multiply(const float *a, const float *b, float *out,
+                              size_t n, int conjugate_b, vs_stream_t stream) {
+  auto s = static_cast<hipStream_t>(stream);
+  VS_REQUIRE(a && b && out, "vs_complex_multiply: null pointer");
+  if (n == 0) return VS_OK;
+  auto ca = reinterpret_cast<const float2 *>(a);
+  auto cb = reinterpret_cast<const float2 *>(b);
+  auto co = reinterpret_cast<float2 *>(out);
+  const bool vec = aligned_to(a, 16) && aligned_to(b, 16) && aligned_to(out, 16);
+  const unsigned grid = elementwise_grid(vec ? n / 2 + 1 : n, kBlock);
+  if (conjugate_b) {
+    if (vec)
+      hipLaunchKernelGGL((cmul_kernel<true, 2>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+    else
+      hipLaunchKernelGGL((cmul_kernel<true, 1>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL((cmul_kernel<false, 2>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+    else
+      hipLaunchKernelGGL((cmul_kernel<false, 1>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+  }
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_complex_conjugate(const float *a, float *out, size_t n,
+                               vs_stream_t stream) {
+  VS_REQUIRE(a && out, "vs_complex_conjugate: null pointer");
+  if (n == 0) return VS_OK;
+  // Reference semantics (arithmetic.h:162-168): pairs (2i, 2i+1) with
+  // 2i+1 < n are conjugated; an odd trailing float is not written.
+  const size_t even = n & ~static_cast<size_t>(1);
+  if (even == 0) return VS_OK;
+  hipLaunchKernelGGL(conj_kernel, dim3(elementwise_grid(even, kBlock)),
+                     dim3(kBlock), 0, static_cast<hipStream_t>(stream), a, out,
+                     even);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_affine(const float *x, float scale, float shift, float *out,
+                    size_t n, vs_stream_t stream) {
+  auto s = static_cast<hipStream_t>(stream);
+  VS_REQUIRE(x && out, "vs_affine: null pointer");
+  // Keep the exact reference arithmetic for the pure scale / pure shift
+  // cases (no fused multiply-add rounding difference).
+  if (shift == 0.f) return launch_map1(x, out, n, ScaleOp{scale}, s);
+  if (scale == 1.f) return launch_map1(x, out, n, ShiftOp{shift}, s);
+  return launch_map1(x, out, n, AffineOp{scale, shift}, s);
+}
+
+vs_status vs_saxpy(float a, const float *x, float *y, size_t n,
+                   vs_stream_t stream) {
+  VS_REQUIRE(x && y, "vs_saxpy: null pointer");
+  return launch_map2(x, static_cast<const float *>(y), y, n, SaxpyOp{a},
+                     static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_fill(float *dst, float value, size_t n, vs_stream_t stream) {
+  VS_REQUIRE(dst, "vs_fill: null pointer");
+  if (n == 0) return VS_OK;
+  hipLaunchKernelGGL(fill_kernel, dim3(elementwise_grid(n / 4 + 1, kBlock)),
+                     dim3(kBlock), 0, static_cast<hipStream_t>(stream), dst,
+                     value, n);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_reverse(const float *src, float *dst, size_t n, int pairs,
+                     vs_stream_t stream) {
+  VS_REQUIRE(src && dst, "vs_reverse: null pointer");
+  VS_REQUIRE(src != dst, "vs_reverse: in-place reversal is not supported");
+  if (n == 0) return VS_OK;
+  auto s = static_cast<hipStream_t>(stream);
+  if (pairs)
+    hipLaunchKernelGGL(reverse_kernel<true>, dim3(elementwise_grid(n / 2, kBlock)),
+                       dim3(kBlock), 0, s, src, dst, n);
+  else
+    hipLaunchKernelGGL(reverse_kernel<false>, dim3(elementwise_grid(n, kBlock)),
+                       dim3(kBlock), 0, s, src, dst, n);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_int16_multiply(const int16_t *a, const int16_t *b, int32_t *out,
+                            size_t n, vs_stream_t stream) {
+  VS_REQUIRE(a && b && out, "vs_int16_multiply: null pointer");
+  return launch_map2(a, b, out, n, Int16MulOp{}, static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_math(int fn, const float *x, float *y, size_t n,
+                  vs_stream_t stream) {
+  auto s = static_cast<hipStream_t>(stream);
+  VS_REQUIRE(x && y, "vs_math: null pointer");
+  switch (fn) {
+    case VS_FN_SIN:
+      return launch_map1(x, y, n, MathOp<VS_FN_SIN>{}, s);
+    case VS_FN_COS:
+      return launch_map1(x, y, n, MathOp<VS_FN_COS>{}, s);
+    case VS_FN_LOG:
+      return launch_map1(x, y, n, MathOp<VS_FN_LOG>{}, s);
+    case VS_FN_EXP:
+      return launch_map1(x, y, n, MathOp<VS_FN_EXP>{}, s);
+  }
+  set_error("vs_math: unknown function %d", fn);
+  return VS_ERR_INVALID;
+}
+
+}  // extern "C"

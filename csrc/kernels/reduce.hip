@@ -1,0 +1,307 @@
+// Reductions and uint8 normalisation.
+//
+// Deterministic two-pass reductions: pass 1 is a grid of at most 1024
+// blocks, each reducing its grid-stride share with 16-byte loads, a
+// wavefront butterfly (__shfl_xor over 64 lanes) and one LDS exchange; pass 2
+// is a single block over the partials.  No float atomics: the result does
+// not depend on dispatch order (cdna_hip_programming.md Guideline 12).
+//
+// Reference counterparts: inc/simd/arithmetic.h:791-808 (sum_elements),
+// src/normalize.c:209-380 (SSE minmax / normalize bodies), :382-443 (scalar).
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "csrc/kernels/device.h"
+#include "csrc/runtime/runtime.h"
+#include "simd/gpu.h"
+
+namespace vs {
+namespace {
+
+constexpr unsigned kBlock = 256;
+constexpr unsigned kMaxPartials = 1024;
+
+struct SumR {
+  using T = float;
+  __device__ static float init() { return 0.f; }
+  __device__ static float op(float a, float b) { return a + b; }
+  __device__ static float wave(float v) { return dev::wave_sum(v); }
+};
+
+// Block reduction of one value per thread; result valid in thread 0.
+template <class R>
+__device__ float block_reduce(float v) {
+  __shared__ float part[kBlock / dev::kWave];
+  v = R::wave(v);
+  const int lane = threadIdx.x & (dev::kWave - 1), wid = threadIdx.x / dev::kWave;
+  if (lane == 0) part[wid] = v;
+  __syncthreads();
+  v = R::init();
+  if (threadIdx.x < blockDim.x / dev::kWave) v = part[threadIdx.x];
+  if (wid == 0) v = R::wave(v);
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void sum_pass1(const float *__restrict__ x,
+                                                    size_t n,
+                                                    float *__restrict__ partial) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  float acc = 0.f;
+  size_t done = 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const size_t n4 = n / 4;
+    const float4 *x4 = reinterpret_cast<const float4 *>(x);
+    for (size_t i = tid; i < n4; i += stride) {
+      const float4 v = x4[i];
+      acc += (v.x + v.y) + (v.z + v.w);
+    }
+    done = n4 * 4;
+  }
+  for (size_t i = done + tid; i < n; i += stride) acc += x[i];
+  acc = block_reduce<SumR>(acc);
+  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void sum_pass2(const float *__restrict__ partial,
+                                                    int np, float *__restrict__ out) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) acc += partial[i];
+  acc = block_reduce<SumR>(acc);
+  if (threadIdx.x == 0) *out = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void minmax_pass1(const float *__restrict__ x,
+                                                       size_t n,
+                                                       float2 *__restrict__ partial) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  float lo = FLT_MAX, hi = -FLT_MAX;
+  // Seed with x[0] so an all-NaN-free array reproduces the scalar result.
+  if (n) lo = hi = x[0];
+  size_t done = 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const size_t n4 = n / 4;
+    const float4 *x4 = reinterpret_cast<const float4 *>(x);
+    for (size_t i = tid; i < n4; i += stride) {
+      const float4 v = x4[i];
+      lo = fminf(lo, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+      hi = fmaxf(hi, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    }
+    done = n4 * 4;
+  }
+  for (size_t i = done + tid; i < n; i += stride) {
+    lo = fminf(lo, x[i]);
+    hi = fmaxf(hi, x[i]);
+  }
+  __shared__ float slo[kBlock / dev::kWave], shi[kBlock / dev::kWave];
+  lo = dev::wave_min(lo);
+  hi = dev::wave_max(hi);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x / 64;
+  if (lane == 0) {
+    slo[wid] = lo;
+    shi[wid] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < static_cast<int>(blockDim.x / 64); w++) {
+      lo = fminf(lo, slo[w]);
+      hi = fmaxf(hi, shi[w]);
+    }
+    partial[blockIdx.x] = make_float2(lo, hi);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void minmax_pass2(const float2 *__restrict__ partial,
+                                                       int np, float *__restrict__ out) {
+  float lo = partial[0].x, hi = partial[0].y;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    lo = fminf(lo, partial[i].x);
+    hi = fmaxf(hi, partial[i].y);
+  }
+  __shared__ float slo[kBlock / 64], shi[kBlock / 64];
+  lo = dev::wave_min(lo);
+  hi = dev::wave_max(hi);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x / 64;
+  if (lane == 0) {
+    slo[wid] = lo;
+    shi[wid] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < static_cast<int>(blockDim.x / 64); w++) {
+      lo = fminf(lo, slo[w]);
+      hi = fmaxf(hi, shi[w]);
+    }
+    out[0] = lo;
+    out[1] = hi;
+  }
+}
+
+// uint8 plane min/max: blocks walk rows, lanes walk 4-byte column groups.
+__global__ __launch_bounds__(kBlock) void minmax2d_pass1(const uint8_t *__restrict__ src,
+                                                         int stride, int w, int h,
+                                                         uint2 *__restrict__ partial) {
+  unsigned lo = 255, hi = 0;
+  for (int y = blockIdx.x; y < h; y += gridDim.x) {
+    const uint8_t *row = src + static_cast<size_t>(y) * stride;
+    const int head = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(row) & 3)) & 3);
+    const int hcount = head < w ? head : w;
+    for (int x = threadIdx.x; x < hcount; x += blockDim.x) {
+      lo = min(lo, static_cast<unsigned>(row[x]));
+      hi = max(hi, static_cast<unsigned>(row[x]));
+    }
+    const int nv = (w - hcount) / 4;
+    const uchar4 *r4 = reinterpret_cast<const uchar4 *>(row + hcount);
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) {
+      const uchar4 v = r4[i];
+      lo = min(lo, min(min(static_cast<unsigned>(v.x), static_cast<unsigned>(v.y)),
+                       min(static_cast<unsigned>(v.z), static_cast<unsigned>(v.w))));
+      hi = max(hi, max(max(static_cast<unsigned>(v.x), static_cast<unsigned>(v.y)),
+                       max(static_cast<unsigned>(v.z), static_cast<unsigned>(v.w))));
+    }
+    for (int x = hcount + nv * 4 + threadIdx.x; x < w; x += blockDim.x) {
+      lo = min(lo, static_cast<unsigned>(row[x]));
+      hi = max(hi, static_cast<unsigned>(row[x]));
+    }
+  }
+  __shared__ unsigned slo[kBlock], shi[kBlock];
+  slo[threadIdx.x] = lo;
+  shi[threadIdx.x] = hi;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (static_cast<int>(threadIdx.x) < s) {
+      slo[threadIdx.x] = min(slo[threadIdx.x], slo[threadIdx.x + s]);
+      shi[threadIdx.x] = max(shi[threadIdx.x], shi[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = make_uint2(slo[0], shi[0]);
+}
+
+__global__ __launch_bounds__(kBlock) void minmax2d_pass2(const uint2 *__restrict__ partial,
+                                                         int np, uint8_t *__restrict__ out) {
+  __shared__ unsigned slo[kBlock], shi[kBlock];
+  unsigned lo = 255, hi = 0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    lo = min(lo, partial[i].x);
+    hi = max(hi, partial[i].y);
+  }
+  slo[threadIdx.x] = lo;
+  shi[threadIdx.x] = hi;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (static_cast<int>(threadIdx.x) < s) {
+      slo[threadIdx.x] = min(slo[threadIdx.x], slo[threadIdx.x + s]);
+      shi[threadIdx.x] = max(shi[threadIdx.x], shi[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = static_cast<uint8_t>(slo[0]);
+    out[1] = static_cast<uint8_t>(shi[0]);
+  }
+}
+
+// dst = (src - min) / ((max - min) / 2) - 1, same operation order as the
+// scalar reference so results agree to the last bit.
+__global__ __launch_bounds__(kBlock) void normalize2d_kernel(
+    const uint8_t *__restrict__ src, int sstride, int w, int h,
+    const uint8_t *__restrict__ mm, int vmin, int vmax, float *__restrict__ dst,
+    int dstride) {
+  const int lo = mm ? mm[0] : vmin;
+  const int hi = mm ? mm[1] : vmax;
+  const bool flat = hi == lo;
+  const float diff = (hi - lo) / 2.f;
+  for (int y = blockIdx.y; y < h; y += gridDim.y) {
+    const uint8_t *srow = src + static_cast<size_t>(y) * sstride;
+    float *drow = dst + static_cast<size_t>(y) * dstride;
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < w;
+         x += gridDim.x * blockDim.x) {
+      drow[x] = flat ? 0.f : (srow[x] - lo) / diff - 1.0f;
+    }
+  }
+}
+
+unsigned partial_count(size_t n) {
+  size_t g = (n + kBlock * 4 - 1) / (kBlock * 4);
+  if (g > kMaxPartials) g = kMaxPartials;
+  if (g == 0) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+}  // namespace
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" {
+
+vs_status vs_sum(const float *x, size_t n, float *out, vs_stream_t stream) {
+  VS_REQUIRE(x && out, "vs_sum: null pointer");
+  auto s = static_cast<hipStream_t>(stream);
+  if (n == 0) {
+    VS_HIP(hipMemsetAsync(out, 0, sizeof(float), s));
+    return VS_OK;
+  }
+  const unsigned g = partial_count(n);
+  DeviceBuffer part;
+  VS_TRY(part.alloc(g * sizeof(float), s));
+  hipLaunchKernelGGL(sum_pass1, dim3(g), dim3(kBlock), 0, s, x, n, part.as<float>());
+  hipLaunchKernelGGL(sum_pass2, dim3(1), dim3(kBlock), 0, s, part.as<float>(),
+                     static_cast<int>(g), out);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_minmax(const float *x, size_t n, float *out, vs_stream_t stream) {
+  VS_REQUIRE(x && out && n > 0, "vs_minmax: invalid arguments");
+  auto s = static_cast<hipStream_t>(stream);
+  const unsigned g = partial_count(n);
+  DeviceBuffer part;
+  VS_TRY(part.alloc(g * sizeof(float2), s));
+  hipLaunchKernelGGL(minmax_pass1, dim3(g), dim3(kBlock), 0, s, x, n,
+                     part.as<float2>());
+  hipLaunchKernelGGL(minmax_pass2, dim3(1), dim3(kBlock), 0, s,
+                     part.as<float2>(), static_cast<int>(g), out);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_minmax2d_u8(const uint8_t *src, int stride, int w, int h,
+                         uint8_t *out, vs_stream_t stream) {
+  VS_REQUIRE(src && out && w > 0 && h > 0 && stride >= w,
+             "vs_minmax2d_u8: invalid arguments (w=%d h=%d stride=%d)", w, h,
+             stride);
+  auto s = static_cast<hipStream_t>(stream);
+  const unsigned g = static_cast<unsigned>(h < static_cast<int>(kMaxPartials) ? h : kMaxPartials);
+  DeviceBuffer part;
+  VS_TRY(part.alloc(g * sizeof(uint2), s));
+  hipLaunchKernelGGL(minmax2d_pass1, dim3(g), dim3(kBlock), 0, s, src, stride, w,
+                     h, part.as<uint2>());
+  hipLaunchKernelGGL(minmax2d_pass2, dim3(1), dim3(kBlock), 0, s,
+                     part.as<uint2>(), static_cast<int>(g), out);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_normalize2d_u8(const uint8_t *src, int sstride, int w, int h,
+                            const uint8_t *mm, int vmin, int vmax, float *dst,
+                            int dstride, vs_stream_t stream) {
+  VS_REQUIRE(src && dst && w > 0 && h > 0 && sstride >= w && dstride >= w,
+             "vs_normalize2d_u8: invalid arguments");
+  VS_REQUIRE(mm || vmin <= vmax, "vs_normalize2d_u8: min > max");
+  const unsigned gx = static_cast<unsigned>((w + kBlock - 1) / kBlock);
+  unsigned gy = static_cast<unsigned>(h);
+  if (gy > 4096) gy = 4096;
+  hipLaunchKernelGGL(normalize2d_kernel, dim3(gx, gy), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), src, sstride, w, h, mm,
+                     vmin, vmax, dst, dstride);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+}  // extern "C"

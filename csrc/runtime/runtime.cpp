@@ -1,0 +1,206 @@
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include "csrc/runtime/runtime.h"
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace vs {
+
+namespace {
+thread_local std::string g_error;
+
+int env_int(const char *name, int dflt) {
+  const char *v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return std::atoi(v);
+}
+}  // namespace
+
+void set_error(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_error = buf;
+  log(2, "error: %s", buf);
+}
+
+void clear_error() { g_error.clear(); }
+const char *last_error() { return g_error.c_str(); }
+
+vs_status hip_status(hipError_t e, const char *what, const char *file,
+                     int line) {
+  set_error("%s: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+  return VS_ERR_HIP;
+}
+
+void fatal(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  std::fprintf(stderr, "veles.simd: fatal: %s\n", buf);
+  std::fflush(stderr);
+  std::abort();
+}
+
+int log_level() {
+  static const int level = env_int("VELES_LOG_LEVEL", 0);
+  return level;
+}
+
+void log(int level, const char *fmt, ...) {
+  if (level > log_level()) return;
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  std::fprintf(stderr, "[veles.simd] %s\n", buf);
+}
+
+int device_count() {
+  static const int count = [] {
+    if (env_int("VELES_DISABLE_GPU", 0)) return 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+      (void)hipGetLastError();
+      n = 0;
+    }
+    return n;
+  }();
+  return count;
+}
+
+bool gpu_available() { return device_count() > 0; }
+
+hipStream_t library_stream() {
+  static std::mutex mu;
+  static std::vector<hipStream_t> streams;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (streams.size() <= static_cast<size_t>(dev))
+    streams.resize(dev + 1, nullptr);
+  if (!streams[dev]) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+      fatal("cannot create the library stream on device %d", dev);
+    streams[dev] = s;
+  }
+  return streams[dev];
+}
+
+bool is_device_pointer(const void *p) {
+  if (!p || !gpu_available()) return false;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice ||
+         attr.type == hipMemoryTypeManaged;
+}
+
+size_t gpu_min_elems() {
+  static const size_t n = [] {
+    const char *v = std::getenv("VELES_GPU_MIN_ELEMS");
+    if (!v || !*v) return static_cast<size_t>(1) << 20;
+    return static_cast<size_t>(std::strtoull(v, nullptr, 10));
+  }();
+  return n;
+}
+
+unsigned elementwise_grid(size_t work_items, unsigned block) {
+  // 256 CUs x 8 resident 256-thread blocks; grid-stride the rest.
+  const size_t cap = 2048;
+  size_t g = (work_items + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+vs_status DeviceBuffer::alloc(size_t bytes, hipStream_t stream) {
+  release();
+  stream_ = stream;
+  bytes_ = bytes;
+  if (bytes == 0) return VS_OK;
+  hipError_t e = hipMallocAsync(&ptr_, bytes, stream);
+  if (e != hipSuccess) {
+    ptr_ = nullptr;
+    bytes_ = 0;
+    set_error("hipMallocAsync(%zu bytes): %s", bytes, hipGetErrorString(e));
+    return VS_ERR_ALLOC;
+  }
+  return VS_OK;
+}
+
+void DeviceBuffer::release() {
+  if (ptr_) (void)hipFreeAsync(ptr_, stream_);
+  ptr_ = nullptr;
+  bytes_ = 0;
+}
+
+Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)
+    : user_(const_cast<void *>(user)), bytes_(bytes), dir_(dir),
+      stream_(stream) {
+  if (is_device_pointer(user)) {
+    dev_ = user_;
+    return;
+  }
+  status_ = buf_.alloc(bytes, stream);
+  if (status_ != VS_OK) return;
+  dev_ = buf_.get();
+  if ((dir & kIn) && bytes) {
+    hipError_t e =
+        hipMemcpyAsync(dev_, user_, bytes, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess)
+      status_ = hip_status(e, "stage-in hipMemcpyAsync", __FILE__, __LINE__);
+  }
+}
+
+vs_status Staged::finish() {
+  if (status_ != VS_OK) return status_;
+  if (dev_ == user_ || !(dir_ & kOut) || !bytes_) return VS_OK;
+  VS_HIP(hipMemcpyAsync(user_, dev_, bytes_, hipMemcpyDeviceToHost, stream_));
+  return VS_OK;
+}
+
+}  // namespace vs
+
+extern "C" {
+
+const char *vs_version(void) { return "0.1.0"; }
+int vs_gpu_available(void) { return vs::gpu_available() ? 1 : 0; }
+int vs_device_count(void) { return vs::device_count(); }
+int vs_set_device(int device) {
+  if (device < 0 || device >= vs::device_count()) {
+    vs::set_error("vs_set_device(%d): %d device(s) visible", device,
+                  vs::device_count());
+    return VS_ERR_INVALID;
+  }
+  VS_HIP(hipSetDevice(device));
+  return VS_OK;
+}
+int vs_get_device(void) {
+  int d = -1;
+  if (!vs::gpu_available() || hipGetDevice(&d) != hipSuccess) return -1;
+  return d;
+}
+const char *vs_last_error(void) { return vs::last_error(); }
+int vs_is_device_pointer(const void *ptr) {
+  return vs::is_device_pointer(ptr) ? 1 : 0;
+}
+vs_status vs_stream_synchronize(vs_stream_t stream) {
+  VS_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  return VS_OK;
+}
+int vs_compiled_arch(void) { return 950; }
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+// Runtime services shared by every API layer: device discovery, error
+// reporting, stream-ordered scratch memory, host<->device staging, logging.
+//
+// The reference has no runtime (everything is a synchronous host call,
+// SURVEY.md §3); this layer is what lets the source-compatible host API drive
+// MI355X kernels: it decides where a call runs, stages host operands through
+// the library's own non-blocking stream and synchronises before returning.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "simd/gpu.h"
+
+namespace vs {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void clear_error();
+const char *last_error();
+
+// Returns VS_ERR_HIP (and records the message) if e != hipSuccess.
+vs_status hip_status(hipError_t e, const char *what, const char *file,
+                     int line);
+#define VS_HIP(expr)                                                    \
+  do {                                                                  \
+    hipError_t vs_e_ = (expr);                                          \
+    if (vs_e_ != hipSuccess)                                            \
+      return ::vs::hip_status(vs_e_, #expr, __FILE__, __LINE__);        \
+  } while (0)
+#define VS_TRY(expr)                    \
+  do {                                          \
+    vs_status vs_s_ = (expr);                   \
+    if (vs_s_ != VS_OK) return vs_s_;           \
+  } while (0)
+#define VS_REQUIRE(cond, ...)            \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::vs::set_error(__VA_ARGS__);      \
+      return VS_ERR_INVALID;             \
+    }                                    \
+  } while (0)
+
+// Aborts with a message; used by the void-returning reference-compatible
+// host API, whose contract is assert() on misuse (e.g. src/matrix.c:300).
+[[noreturn]] void fatal(const char *fmt, ...)
+    __attribute__((format(printf, 1, 2)));
+#define VS_CHECK_API(expr)                                              \
+  do {                                                                  \
+    vs_status vs_s_ = (expr);                                           \
+    if (vs_s_ != VS_OK)                                                 \
+      ::vs::fatal("%s failed: %s", #expr, ::vs::last_error());          \
+  } while (0)
+
+// --------------------------------------------------------------- logging
+// VELES_LOG_LEVEL: 0 quiet (default), 1 dispatch decisions, 2 verbose.
+int log_level();
+void log(int level, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+
+// ---------------------------------------------------------------- device
+bool gpu_available();
+int device_count();
+// Library stream of the current device (non-blocking, created lazily).
+hipStream_t library_stream();
+bool is_device_pointer(const void *p);
+// Elements from which host-pointer array ops go to the GPU
+// (VELES_GPU_MIN_ELEMS, default 1 << 20).
+size_t gpu_min_elems();
+// Launch helper: grid size for a grid-stride elementwise kernel.
+unsigned elementwise_grid(size_t work_items, unsigned block);
+
+// ------------------------------------------------------- scratch memory
+// Stream-ordered device allocation (hipMallocAsync); freed on destruction
+// with hipFreeAsync on the same stream.
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  DeviceBuffer(size_t bytes, hipStream_t stream) { alloc(bytes, stream); }
+  ~DeviceBuffer() { release(); }
+  DeviceBuffer(const DeviceBuffer &) = delete;
+  DeviceBuffer &operator=(const DeviceBuffer &) = delete;
+  DeviceBuffer(DeviceBuffer &&o) noexcept { *this = std::move(o); }
+  DeviceBuffer &operator=(DeviceBuffer &&o) noexcept {
+    release();
+    ptr_ = o.ptr_;
+    bytes_ = o.bytes_;
+    stream_ = o.stream_;
+    o.ptr_ = nullptr;
+    o.bytes_ = 0;
+    return *this;
+  }
+  vs_status alloc(size_t bytes, hipStream_t stream);
+  void release();
+  template <class T>
+  T *as() const {
+    return static_cast<T *>(ptr_);
+  }
+  void *get() const { return ptr_; }
+  size_t bytes() const { return bytes_; }
+
+ private:
+  void *ptr_ = nullptr;
+  size_t bytes_ = 0;
+  hipStream_t stream_ = nullptr;
+};
+
+// ----------------------------------------------------------- staging
+// Presents a host-or-device operand as a device pointer on `stream`.
+// Device pointers pass through; host buffers are copied in (kIn), out on
+// finish() (kOut) or both.
+class Staged {
+ public:
+  enum Dir { kIn = 1, kOut = 2, kInOut = 3 };
+  Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream);
+  vs_status status() const { return status_; }
+  template <class T>
+  T *dev() const {
+    return static_cast<T *>(dev_);
+  }
+  // Copies device results back to the host buffer (kOut / kInOut).
+  vs_status finish();
+
+ private:
+  void *user_;
+  void *dev_ = nullptr;
+  size_t bytes_;
+  Dir dir_;
+  hipStream_t stream_;
+  DeviceBuffer buf_;
+  vs_status status_ = VS_OK;
+};
+
+}  // namespace vs

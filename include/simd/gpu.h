@@ -1,0 +1,188 @@
+/*! @file gpu.h
+ *  @brief Device-pointer, batched and stream-ordered API (no reference
+ *  counterpart; SURVEY.md App. B "New").
+ *
+ *  Every vs_* compute function takes device pointers and a stream (a
+ *  hipStream_t passed as void*; NULL is the HIP null stream) and is
+ *  asynchronous with respect to the host: it only enqueues work.  Temporary
+ *  device memory is taken from the stream-ordered pool (hipMallocAsync), so
+ *  the calls are safe to use from several streams and to capture in graphs
+ *  once their plans (FFT twiddles, filters) exist.
+ *
+ *  This is the layer the PyTorch custom ops (veles.simd_amd.ops) and the
+ *  multi-GPU layer (veles.simd_amd.parallel) call; the source-compatible C
+ *  API in the other headers is built on it.
+ *  Copyright 2026 veles.simd_amd authors. Apache-2.0.
+ */
+#ifndef VELES_SIMD_GPU_H_
+#define VELES_SIMD_GPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+#include <simd/common.h>
+
+SIMD_API_BEGIN
+
+typedef void *vs_stream_t;
+
+typedef enum {
+  VS_OK = 0,
+  VS_ERR_INVALID = 1,      ///< bad argument (message in vs_last_error())
+  VS_ERR_HIP = 2,          ///< HIP runtime error
+  VS_ERR_NO_GPU = 3,       ///< no usable gfx950 device
+  VS_ERR_UNSUPPORTED = 4,  ///< shape/parameter outside what is implemented
+  VS_ERR_ALLOC = 5         ///< allocation failure
+} vs_status;
+
+typedef enum {
+  VS_F32 = 0,
+  VS_F16 = 1,  ///< IEEE binary16 stored as uint16
+  VS_I16 = 2,
+  VS_I32 = 3,
+  VS_U8 = 4
+} vs_dtype;
+
+/* ---------------------------------------------------------------- runtime */
+const char *vs_version(void);
+/// 1 if at least one HIP device is usable (VELES_DISABLE_GPU=1 forces 0).
+int vs_gpu_available(void);
+int vs_device_count(void);
+int vs_set_device(int device);
+int vs_get_device(void);
+/// Message of the last failing call on this thread ("" if none).
+const char *vs_last_error(void);
+int vs_is_device_pointer(const void *ptr);
+vs_status vs_stream_synchronize(vs_stream_t stream);
+/// Number of the architecture the kernels were compiled for (950).
+int vs_compiled_arch(void);
+
+/* ----------------------------------------------------------- elementwise */
+typedef enum { VS_OP_ADD = 0, VS_OP_SUB = 1, VS_OP_MUL = 2 } vs_binary_op;
+typedef enum {
+  VS_FN_SIN = 0,
+  VS_FN_COS = 1,
+  VS_FN_LOG = 2,
+  VS_FN_EXP = 3
+} vs_math_fn;
+
+/// dst[i] = convert(src[i]); float->int truncates, narrowing saturates.
+vs_status vs_convert(const void *src, int src_dtype, void *dst, int dst_dtype,
+                     size_t n, vs_stream_t stream);
+vs_status vs_binary(int op, const float *a, const float *b, float *out,
+                    size_t n, vs_stream_t stream);
+/// out = a * b (or a * conj(b)) over n interleaved complex numbers.
+vs_status vs_complex_multiply(const float *a, const float *b, float *out,
+                              size_t n_complex, int conjugate_b,
+                              vs_stream_t stream);
+/// Conjugates n_floats/2 interleaved complex numbers (odd tail copied).
+vs_status vs_complex_conjugate(const float *a, float *out, size_t n_floats,
+                               vs_stream_t stream);
+/// out = x * scale + shift.
+vs_status vs_affine(const float *x, float scale, float shift, float *out,
+                    size_t n, vs_stream_t stream);
+/// y = a * x + y.
+vs_status vs_saxpy(float a, const float *x, float *y, size_t n,
+                   vs_stream_t stream);
+vs_status vs_fill(float *dst, float value, size_t n, vs_stream_t stream);
+/// dst[i] = src[n-1-i] (complex_pairs: reverse order of float pairs).
+vs_status vs_reverse(const float *src, float *dst, size_t n, int complex_pairs,
+                     vs_stream_t stream);
+vs_status vs_int16_multiply(const int16_t *a, const int16_t *b, int32_t *out,
+                            size_t n, vs_stream_t stream);
+vs_status vs_math(int fn, const float *x, float *y, size_t n,
+                  vs_stream_t stream);
+
+/* ------------------------------------------------------------ reductions */
+/// *out_dev = sum(x) (pairwise tree in fp32).
+vs_status vs_sum(const float *x, size_t n, float *out_dev, vs_stream_t stream);
+/// out_dev[0] = min, out_dev[1] = max.
+vs_status vs_minmax(const float *x, size_t n, float *out_dev,
+                    vs_stream_t stream);
+vs_status vs_minmax2d_u8(const uint8_t *src, int src_stride, int width,
+                         int height, uint8_t *out_dev, vs_stream_t stream);
+/// If minmax_dev != NULL the bounds are read from it (fused normalize2D),
+/// otherwise (vmin, vmax) are used.
+vs_status vs_normalize2d_u8(const uint8_t *src, int src_stride, int width,
+                            int height, const uint8_t *minmax_dev, int vmin,
+                            int vmax, float *dst, int dst_stride,
+                            vs_stream_t stream);
+
+/* ------------------------------------------------------------------ GEMM */
+/// C = alpha * op(A) * op(B) + beta * C, row-major, exact fp32 (MFMA f32).
+/// op(A) is M x K, op(B) is K x N.  trans flags: 0 = as stored, 1 = transposed.
+vs_status vs_sgemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                   const float *a, int64_t lda, const float *b, int64_t ldb,
+                   float beta, float *c, int64_t ldc, vs_stream_t stream);
+vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
+                                   int k, float alpha, const float *a,
+                                   int64_t lda, int64_t stride_a,
+                                   const float *b, int64_t ldb,
+                                   int64_t stride_b, float beta, float *c,
+                                   int64_t ldc, int64_t stride_c, int batch,
+                                   vs_stream_t stream);
+
+/* ------------------------------------------------------------------- FFT */
+/// Unnormalised complex FFT of `batch` contiguous interleaved signals of n
+/// (power of two, 2..2^24) points.  inverse=0: exp(-2 pi i jk/n).
+vs_status vs_fft_c2c(const float *in, float *out, int n, int batch,
+                     int inverse, vs_stream_t stream);
+/// Real forward FFT: n real -> n/2+1 complex (n+2 floats) per signal.
+vs_status vs_fft_r2c(const float *in, float *out, int n, int batch,
+                     vs_stream_t stream);
+/// Real inverse FFT (unnormalised): n/2+1 complex -> n real per signal.
+vs_status vs_fft_c2r(const float *in, float *out, int n, int batch,
+                     vs_stream_t stream);
+
+/* ----------------------------------------------------------- convolution */
+typedef enum {
+  VS_CONV_AUTO = 0,
+  VS_CONV_DIRECT = 1,
+  VS_CONV_FFT = 2,
+  VS_CONV_OVERLAP_SAVE = 3
+} vs_conv_algo;
+
+/// Batched full linear convolution (correlate=0) or cross-correlation
+/// (correlate=1): y[b] (length x_len + h_len - 1, row stride y_stride) of
+/// x[b] (stride x_stride) with h[b] (stride h_stride; 0 = one shared filter).
+vs_status vs_conv1d(int algo, int correlate, const float *x, int x_len,
+                    int64_t x_stride, const float *h, int h_len,
+                    int64_t h_stride, float *y, int64_t y_stride, int batch,
+                    vs_stream_t stream);
+/// Algorithm VS_CONV_AUTO resolves to for this shape.
+int vs_conv1d_select(int x_len, int h_len, int batch);
+/// Overlap-save block length the library uses for filter length h_len.
+int vs_conv1d_os_block(int h_len);
+
+/* -------------------------------------------------------------- wavelets */
+/// Batched single-level decimated DWT: hi/lo rows of len/2 (stride
+/// out_stride) per input row (stride src_stride).
+vs_status vs_dwt(int type, int order, int ext, const float *src, int len,
+                 int64_t src_stride, float *hi, float *lo, int64_t out_stride,
+                 int batch, vs_stream_t stream);
+/// Batched single-level stationary DWT at `level` (full-length outputs).
+vs_status vs_swt(int type, int order, int level, int ext, const float *src,
+                 int len, int64_t src_stride, float *hi, float *lo,
+                 int64_t out_stride, int batch, vs_stream_t stream);
+/// Fused `levels`-level stationary DWT, level l fed by level l-1's lo:
+/// hi is [batch][levels][len], lo is [batch][len] (the last level's lo).
+vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
+                            const float *src, int len, float *hi, float *lo,
+                            int batch, vs_stream_t stream);
+/// Fused `levels`-level decimated DWT (Mallat pyramid); per row of out
+/// (length len): [hi_1 (len/2) | hi_2 (len/4) | ... | hi_L | lo_L].
+vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,
+                            const float *src, int len, float *out, int batch,
+                            vs_stream_t stream);
+/// Copies the float low-pass filter (order taps) into host memory `out`.
+vs_status vs_wavelet_filter(int type, int order, float *out);
+
+/* ----------------------------------------------------------------- peaks */
+/// Ordered strict extrema of x[0..n): positions/values of the first
+/// `capacity` go to pos_dev/val_dev, the total count to *count_dev.
+vs_status vs_detect_peaks(const float *x, size_t n, int type, int *pos_dev,
+                          float *val_dev, size_t capacity,
+                          unsigned long long *count_dev, vs_stream_t stream);
+
+SIMD_API_END
+
+#endif  // VELES_SIMD_GPU_H_

@@ -1,0 +1,27 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running test")
+    # Build the native library once if this checkout does not have it yet.
+    from veles.simd_amd import _lib, build
+    if not os.path.exists(_lib.LIB_PATH):
+        build.build()
+
+
+def pytest_collection_modifyitems(config, items):
+    from veles.simd_amd import _lib
+    if _lib.gpu_available():
+        return
+    skip = pytest.mark.skip(reason="no GPU visible to the native library")
+    for item in items:
+        if "gpu" in item.keywords:
+            item.add_marker(skip)

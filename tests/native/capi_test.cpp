@@ -1,0 +1,128 @@
+// Native C API test: compiles against include/simd/*.h exactly as a user of
+// the reference would (source compatibility) and re-checks the reference's
+// golden vectors (tests/*.cc of the reference) through the public symbols.
+// Runs host paths everywhere and the GPU paths when a device is visible.
+// Usage: capi_test [--list] [name-substring]
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include <simd/arithmetic.h>
+#include <simd/gpu.h>
+#include <simd/mathfun.h>
+#include <simd/matrix.h>
+#include <simd/memory.h>
+#include <simd/normalize.h>
+
+#include "mini_test.h"
+
+TEST_CASE(memory_align_complement) {
+  alignas(32) float f[32];
+  alignas(32) int16_t s[32];
+  CHECK_EQ(0, align_complement_f32(f));
+  CHECK_EQ(7, align_complement_f32(&f[1]));
+  CHECK_EQ(1, align_complement_f32(&f[7]));
+  CHECK_EQ(15, align_complement_i16(&s[1]));
+  CHECK_EQ(0, align_complement_i16(&s[16]));
+}
+
+TEST_CASE(memory_alloc_and_pad) {
+  void *p = malloc_aligned(100);
+  CHECK_EQ(0u, reinterpret_cast<uintptr_t>(p) % 64);
+  free(p);
+  char *q = static_cast<char *>(malloc_aligned_offset(100, 3));
+  CHECK_EQ(3u, reinterpret_cast<uintptr_t>(q) % 64);
+  free(q - 3);
+  float orig[100];
+  memsetf(orig, 1.f, 100);
+  size_t nl = 0;
+  float *z = zeropadding(orig, 100, &nl);
+  CHECK_EQ(256u, nl);
+  for (int i = 0; i < 100; i++) CHECK_EQ(1.f, z[i]);
+  for (int i = 100; i < 256; i++) CHECK_EQ(0.f, z[i]);
+  free(z);
+  float src[25], dst[25];
+  for (int i = 0; i < 25; i++) src[i] = i;
+  rmemcpyf(dst + 1, src + 1, 24);
+  for (int i = 1; i < 25; i++) CHECK_EQ(dst[i], src[25 - i]);
+}
+
+TEST_CASE(arithmetic_goldens) {
+  float a[8] = {1, 2, 3, 4, 5, 6, 7, 8};
+  float b[8] = {-1.5f, 1, 3.5f, 3, -5.5f, 6.5f, 2, -9};
+  float r[8], v[8];
+  complex_multiply(a, b, r);
+  for (int i = 0; i < 8; i += 2) complex_multiply_na(a + i, b + i, v + i);
+  CHECK(memcmp(r, v, sizeof(r)) == 0);
+  uint16_t h[] = {12288, 16777, 18103, 49820};
+  float hf[4];
+  float16_to_float(h, 4, hf);
+  CHECK_NEAR(0.125f, hf[0], 1e-6);
+  CHECK_NEAR(2.76757812f, hf[1], 1e-5);
+  CHECK_NEAR(-3.3046875f, hf[3], 1e-5);
+  CHECK_EQ(128, next_highest_power_of_2(100));
+}
+
+TEST_CASE(matrix_multiply_golden) {
+  const float m1[6] = {1, 2, 3, -2, 0, 4};
+  const float m2[12] = {0, 1, 3, -2, 5, -1, 2, 4, -3, 0, -4, 2};
+  const float valid[8] = {1, -1, -5, 12, -12, -2, -22, 12};
+  for (int simd = 0; simd < 2; simd++) {
+    float res[8];
+    matrix_multiply(simd, m1, m2, 3, 2, 4, 3, res);
+    for (int i = 0; i < 8; i++) CHECK_NEAR(valid[i], res[i], 0.01);
+  }
+}
+
+TEST_CASE(matrix_multiply_odd_vs_scalar) {
+  // tests/matrix.cc: 299x125 * 125x999 (odd everything), tolerance 0.1
+  const int w1 = 125, h1 = 299, w2 = 999;
+  std::vector<float> m1(w1 * h1), m2(w2 * w1), r0(h1 * w2), r1(h1 * w2);
+  for (int i = 0; i < h1; i++)
+    for (int j = 0; j < w1; j++) m1[i * w1 + j] = -j % 17 + i % 6;
+  for (int i = 0; i < w1; i++)
+    for (int j = 0; j < w2; j++) m2[i * w2 + j] = j % 15 - i % 5;
+  matrix_multiply(0, m1.data(), m2.data(), w1, h1, w2, w1, r0.data());
+  matrix_multiply(1, m1.data(), m2.data(), w1, h1, w2, w1, r1.data());
+  for (size_t i = 0; i < r0.size(); i++) CHECK_NEAR(r0[i], r1[i], 0.1);
+}
+
+TEST_CASE(normalize_golden) {
+  for (int simd = 0; simd < 2; simd++) {
+    std::vector<uint8_t> src(128 * 100, 1);
+    src[0] = 127;
+    src[1] = 15;
+    src[10] = 252;
+    src[89] = 31;
+    src[128 + 21] = 3;
+    std::vector<float> dst(100 * 100);
+    normalize2D(simd, src.data(), 128, 100, 100, dst.data(), 100);
+    CHECK_NEAR(2.f * (127 - 1) / 251 - 1, dst[0], 1e-6);
+    CHECK_NEAR(-1.f, dst[2], 1e-7);
+    CHECK_NEAR(1.f, dst[10], 1e-7);
+    CHECK_NEAR(2.f * (3 - 1) / 251 - 1, dst[121], 1e-6);
+  }
+}
+
+TEST_CASE(mathfun_vs_double) {
+  const int n = 199;
+  float x[n], y[n];
+  for (int i = 0; i < n; i++) x[i] = (float(i % 19) - float(i % 6)) * 1.1f;
+  for (int simd = 0; simd < 2; simd++) {
+    sin_psv(simd, x, n, y);
+    for (int i = 0; i < n; i++)
+      CHECK_NEAR(static_cast<float>(std::sin(double(x[i]))), y[i], 4e-7);
+    exp_psv(simd, x, n, y);
+    for (int i = 0; i < n; i++) {
+      const double e = std::exp(double(x[i]));
+      CHECK_NEAR(1.0, y[i] / e, 5e-7);
+    }
+  }
+}
+
+int main(int argc, char **argv) { return mini_test::run_all(argc, argv); }

@@ -1,0 +1,140 @@
+"""Port of the reference tests/matrix.cc (goldens + MatrixTest sweep) plus
+GPU-vs-fp64 checks of the MFMA SGEMM."""
+import numpy as np
+import pytest
+
+from veles.simd_amd import capi
+
+
+def _fixture(w1, h1, w2, h2):
+    # tests/matrix.cc:39-51: m1[i][j] = -j % 17 + i % 6, m2 = j % 15 - i % 5
+    # (C semantics of -j % 17: the remainder keeps the sign of -j).
+    i1, j1 = np.meshgrid(np.arange(h1), np.arange(w1), indexing="ij")
+    m1 = (-(j1 % 17) + i1 % 6).astype(np.float32)
+    i2, j2 = np.meshgrid(np.arange(h2), np.arange(w2), indexing="ij")
+    m2 = (j2 % 15 - i2 % 5).astype(np.float32)
+    return m1.ravel(), m2.ravel()
+
+
+def test_add_validate():
+    m1 = [1, 2, 3, -2, 0, 4]
+    m2 = [0, 1, 3, 5, -1, 2]
+    np.testing.assert_allclose(capi.matrix_add(0, m1, m2, 3, 2),
+                               [1, 3, 6, 3, -1, 6], atol=0.01)
+
+
+def test_sub_validate():
+    m1 = [1, 2, 3, -2, 0, 4]
+    m2 = [0, 1, 3, 5, -1, 2]
+    np.testing.assert_allclose(capi.matrix_sub(0, m1, m2, 3, 2),
+                               [1, 1, 0, -7, 1, 2], atol=0.01)
+
+
+VALID = [1, -1, -5, 12, -12, -2, -22, 12]
+
+
+@pytest.mark.parametrize("simd", [0, 1])
+def test_multiply_validate(simd):
+    m1 = [1, 2, 3, -2, 0, 4]
+    m2 = [0, 1, 3, -2, 5, -1, 2, 4, -3, 0, -4, 2]
+    np.testing.assert_allclose(capi.matrix_multiply(simd, m1, m2, 3, 2, 4, 3),
+                               VALID, atol=0.01)
+
+
+@pytest.mark.parametrize("simd", [0, 1])
+def test_multiply_transposed_validate(simd):
+    m1 = [1, 2, 3, -2, 0, 4]
+    m2 = [0, 5, -3, 1, -1, 0, 3, 2, -4, -2, 4, 2]
+    np.testing.assert_allclose(
+        capi.matrix_multiply_transposed(simd, m1, m2, 3, 2, 3, 4), VALID,
+        atol=0.01)
+
+
+SWEEP = ([(d, d, d, d) for d in (1, 3, 99)] +
+         [(128, 300, 1000, 128), (125, 299, 999, 125)])
+
+
+@pytest.mark.parametrize("dims", SWEEP)
+@pytest.mark.parametrize("kind", ["add", "sub", "mul", "mulT"])
+def test_matrix_sweep(dims, kind):
+    w1, h1, w2, h2 = dims
+    if kind in ("add", "sub") and dims[0] == 128:
+        pytest.skip("reference sweeps add/sub on the square sizes and 125x299")
+    if kind == "mulT":
+        w2, h2 = h2, w2
+    m1, m2 = _fixture(w1, h1, w2, h2)
+    if kind == "add":
+        base = capi.matrix_add(0, m1, m2, w1, h1)
+        simd = capi.matrix_add(1, m1, m2, w1, h1)
+    elif kind == "sub":
+        base = capi.matrix_sub(0, m1, m2, w1, h1)
+        simd = capi.matrix_sub(1, m1, m2, w1, h1)
+    elif kind == "mul":
+        base = capi.matrix_multiply(0, m1, m2, w1, h1, w2, h2)
+        simd = capi.matrix_multiply(1, m1, m2, w1, h1, w2, h2)
+    else:
+        base = capi.matrix_multiply_transposed(0, m1, m2, w1, h1, w2, h2)
+        simd = capi.matrix_multiply_transposed(1, m1, m2, w1, h1, w2, h2)
+    np.testing.assert_allclose(simd, base, atol=0.1)
+
+
+def test_add_sub_125x299():
+    m1, m2 = _fixture(125, 299, 125, 299)
+    np.testing.assert_allclose(capi.matrix_add(1, m1, m2, 125, 299),
+                               capi.matrix_add(0, m1, m2, 125, 299), atol=0.1)
+    np.testing.assert_allclose(capi.matrix_sub(1, m1, m2, 125, 299),
+                               capi.matrix_sub(0, m1, m2, 125, 299), atol=0.1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (33, 65, 17), (128, 128, 16),
+                                   (299, 999, 125), (256, 512, 1024),
+                                   (1000, 300, 256)])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_sgemm_gpu_vs_fp64(m, n, k, ta, tb):
+    import torch
+    from veles.simd_amd import ops
+    g = torch.Generator().manual_seed(m * 7 + n * 3 + k)
+    a = torch.rand((k, m) if ta else (m, k), generator=g) * 2 - 1
+    b = torch.rand((n, k) if tb else (k, n), generator=g) * 2 - 1
+    ref = ((a.double().T if ta else a.double()) @ (b.double().T if tb else b.double()))
+    c = ops.sgemm(a.cuda(), b.cuda(), bool(ta), bool(tb)).cpu().double()
+    err = (c - ref).abs().max().item()
+    # exact-fp32 MFMA: error ~1e-7 * sum|a*b| <= 1e-7 * k
+    assert err <= 2e-6 * k + 1e-6, err
+
+
+@pytest.mark.gpu
+def test_sgemm_identity_asymmetric():
+    """A = I with an asymmetric B catches a transposed C/D map."""
+    import torch
+    from veles.simd_amd import ops
+    n = 160
+    b = torch.arange(n * n, dtype=torch.float32).reshape(n, n) / (n * n)
+    c = ops.sgemm(torch.eye(n).cuda(), b.cuda()).cpu()
+    assert torch.equal(c, b)
+
+
+@pytest.mark.gpu
+def test_sgemm_batched_and_alpha():
+    import torch
+    from veles.simd_amd import ops
+    a = torch.randn(5, 70, 90)
+    b = torch.randn(5, 90, 40)
+    c = ops.sgemm(a.cuda(), b.cuda(), alpha=0.5).cpu()
+    torch.testing.assert_close(c, 0.5 * torch.bmm(a.double(), b.double()).float(),
+                               atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_sgemm_autograd():
+    import torch
+    from veles.simd_amd import ops
+    a = torch.randn(37, 45, device="cuda", requires_grad=True)
+    b = torch.randn(45, 29, device="cuda", requires_grad=True)
+    ops.sgemm(a, b).sum().backward()
+    a2 = a.detach().clone().requires_grad_()
+    b2 = b.detach().clone().requires_grad_()
+    (a2 @ b2).sum().backward()
+    torch.testing.assert_close(a.grad, a2.grad, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(b.grad, b2.grad, atol=1e-4, rtol=1e-4)

@@ -1,0 +1,68 @@
+"""Port of reference tests/normalize.cc plus device checks."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from veles.simd_amd import capi
+
+
+def _plane():
+    a = np.ones(128 * 100, np.uint8)
+    a[0], a[1], a[10], a[89], a[128 + 21] = 127, 15, 252, 31, 3
+    return a
+
+
+@pytest.mark.parametrize("simd", [0, 1])
+def test_normalize2d(simd):
+    src = _plane()
+    res = np.zeros(100 * 100, np.float32)
+    capi.fn("normalize2D")(simd, capi.p(src), 128, 100, 100, capi.p(res), 100)
+    f = np.float32
+    assert abs(res[0] - (f(2) * (127 - 1) / 251 - 1)) <= 1e-6
+    np.testing.assert_allclose(res[1], f(2) * (15 - 1) / 251 - 1, rtol=1e-6)
+    assert res[2] == -1.0 and res[10] == 1.0
+    np.testing.assert_allclose(res[89], f(2) * (31 - 1) / 251 - 1, rtol=1e-6)
+    np.testing.assert_allclose(res[121], f(2) * (3 - 1) / 251 - 1, rtol=1e-6)
+
+
+@pytest.mark.parametrize("simd", [0, 1])
+def test_minmax1d(simd):
+    a = np.ones(100, np.float32)
+    a[0], a[1], a[10], a[89], a[21] = 127, 15, 252, 31, 3
+    mn, mx = ctypes.c_float(), ctypes.c_float()
+    capi.fn("minmax1D")(simd, capi.p(a), 100, ctypes.byref(mn), ctypes.byref(mx))
+    assert mx.value == 252 and mn.value == 1
+    capi.fn("minmax1D")(simd, capi.p(a), 100, None, None)
+    mx2 = ctypes.c_float()
+    capi.fn("minmax1D")(simd, capi.p(a), 100, None, ctypes.byref(mx2))
+    assert mx2.value == 252
+
+
+@pytest.mark.parametrize("simd", [0, 1])
+def test_minmax2d_and_flat(simd):
+    src = _plane()
+    mn, mx = ctypes.c_uint8(), ctypes.c_uint8()
+    capi.fn("minmax2D")(simd, capi.p(src), 128, 100, 100, ctypes.byref(mn),
+                        ctypes.byref(mx))
+    assert (mn.value, mx.value) == (1, 252)
+    # max == min: zeros row by row, row padding of dst untouched
+    flat = np.full(64 * 10, 7, np.uint8)
+    dst = np.full(40 * 10, 5.0, np.float32)
+    capi.fn("normalize2D_minmax")(simd, 7, 7, capi.p(flat), 64, 30, 10,
+                                  capi.p(dst), 40)
+    d = dst.reshape(10, 40)
+    assert (d[:, :30] == 0).all() and (d[:, 30:] == 5.0).all()
+
+
+@pytest.mark.gpu
+def test_normalize2d_device_large():
+    import torch
+    from veles.simd_amd import ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(3, 250, (1080, 1923), dtype=torch.uint8, generator=g)
+    got = ops.normalize2d(x.cuda()).cpu()
+    mn, mx = int(x.min()), int(x.max())
+    want = (x.float() - mn) / np.float32((mx - mn) / 2.0) - 1.0
+    torch.testing.assert_close(got, want, atol=0, rtol=0)
+    assert torch.equal(ops.minmax(x.cuda()).cpu(), torch.tensor([mn, mx], dtype=torch.uint8))

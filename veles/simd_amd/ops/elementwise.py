@@ -1,0 +1,283 @@
+"""Elementwise / reduction ops (torch custom ops over the HIP kernels).
+
+Reference: inc/simd/arithmetic.h (conversions, real/complex arithmetic,
+sum_elements, add_to_all), inc/simd/mathfun.h (sin/cos/log/exp),
+src/normalize.c (minmax, normalize2D), src/memory.c (memsetf, rmemcpyf).
+CPU tensors run the same math with torch (the host reference semantics);
+GPU tensors always run the native kernels.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _lib
+from ._util import on_device, ptr, require_gpu_tensor, stream_of
+
+VS_F32, VS_F16, VS_I16, VS_I32, VS_U8 = 0, 1, 2, 3, 4
+_DT = {torch.float32: VS_F32, torch.int16: VS_I16, torch.int32: VS_I32,
+       torch.uint8: VS_U8, torch.float16: VS_F16}
+_FN = {"sin": 0, "cos": 1, "log": 2, "exp": 3}
+_OP = {"add": 0, "sub": 1, "mul": 2}
+
+
+def _gpu(x: torch.Tensor, name: str) -> bool:
+    if x.is_cuda:
+        require_gpu_tensor(x, name)
+        return True
+    return False
+
+
+# ------------------------------------------------------------------ convert
+@torch.library.custom_op("veles::convert", mutates_args=())
+def convert(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Numeric conversion with the library semantics: float -> int truncates
+    toward zero and saturates; int32 -> int16 saturates; float16 inputs may
+    be given as torch.float16 (raw IEEE binary16)."""
+    if not _gpu(x, "veles::convert"):
+        if dtype in (torch.int16, torch.int32) and x.dtype.is_floating_point:
+            info = torch.iinfo(dtype)
+            t = torch.nan_to_num(x.float(), nan=0.0).trunc()
+            return t.clamp(info.min, info.max).to(dtype)
+        if dtype == torch.int16 and x.dtype == torch.int32:
+            return x.clamp(-32768, 32767).to(torch.int16)
+        return x.to(dtype)
+    x = x.contiguous()
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    with on_device(x):
+        _lib.call("vs_convert", ptr(x), _DT[x.dtype], ptr(out), _DT[dtype],
+                  x.numel(), stream_of(x))
+    return out
+
+
+@convert.register_fake
+def _(x, dtype):
+    return torch.empty(x.shape, dtype=dtype, device=x.device)
+
+
+# ------------------------------------------------------------------- binary
+@torch.library.custom_op("veles::binary", mutates_args=())
+def binary(a: torch.Tensor, b: torch.Tensor, op: str) -> torch.Tensor:
+    """a (+|-|*) b elementwise, float32, same shape (matrix_add/sub,
+    real_multiply_array)."""
+    if a.shape != b.shape:
+        raise ValueError("veles::binary: shape mismatch")
+    if not _gpu(a, "veles::binary"):
+        return {"add": torch.add, "sub": torch.sub, "mul": torch.mul}[op](a, b)
+    a, b = a.contiguous(), b.contiguous()
+    out = torch.empty_like(a)
+    with on_device(a):
+        _lib.call("vs_binary", _OP[op], ptr(a), ptr(b), ptr(out), a.numel(),
+                  stream_of(a))
+    return out
+
+
+@binary.register_fake
+def _(a, b, op):
+    return torch.empty_like(a)
+
+
+def add(a, b):
+    return binary(a, b, "add")
+
+
+def sub(a, b):
+    return binary(a, b, "sub")
+
+
+def mul(a, b):
+    return binary(a, b, "mul")
+
+
+# ------------------------------------------------------------------ complex
+@torch.library.custom_op("veles::complex_multiply", mutates_args=())
+def complex_multiply(a: torch.Tensor, b: torch.Tensor,
+                     conjugate_b: bool = False) -> torch.Tensor:
+    """Interleaved complex product over float32 tensors (last dim even)."""
+    if a.shape != b.shape or a.shape[-1] % 2:
+        raise ValueError("veles::complex_multiply: bad shapes")
+    if not _gpu(a, "veles::complex_multiply"):
+        ca = torch.view_as_complex(a.contiguous().view(*a.shape[:-1], -1, 2))
+        cb = torch.view_as_complex(b.contiguous().view(*b.shape[:-1], -1, 2))
+        r = ca * (cb.conj() if conjugate_b else cb)
+        return torch.view_as_real(r).reshape(a.shape)
+    a, b = a.contiguous(), b.contiguous()
+    out = torch.empty_like(a)
+    with on_device(a):
+        _lib.call("vs_complex_multiply", ptr(a), ptr(b), ptr(out),
+                  a.numel() // 2, int(conjugate_b), stream_of(a))
+    return out
+
+
+@complex_multiply.register_fake
+def _(a, b, conjugate_b=False):
+    return torch.empty_like(a)
+
+
+@torch.library.custom_op("veles::complex_conjugate", mutates_args=())
+def complex_conjugate(a: torch.Tensor) -> torch.Tensor:
+    if not _gpu(a, "veles::complex_conjugate"):
+        r = a.clone()
+        r.view(-1)[1::2] *= -1
+        return r
+    a = a.contiguous()
+    out = a.clone()
+    with on_device(a):
+        _lib.call("vs_complex_conjugate", ptr(a), ptr(out), a.numel(),
+                  stream_of(a))
+    return out
+
+
+@complex_conjugate.register_fake
+def _(a):
+    return torch.empty_like(a)
+
+
+# ------------------------------------------------------------------- affine
+@torch.library.custom_op("veles::affine", mutates_args=())
+def affine(x: torch.Tensor, scale: float = 1.0, shift: float = 0.0) -> torch.Tensor:
+    """x * scale + shift (real_multiply_scalar / add_to_all)."""
+    if not _gpu(x, "veles::affine"):
+        if shift == 0.0:
+            return x * scale
+        if scale == 1.0:
+            return x + shift
+        return x * scale + shift
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    with on_device(x):
+        _lib.call("vs_affine", ptr(x), float(scale), float(shift), ptr(out),
+                  x.numel(), stream_of(x))
+    return out
+
+
+@affine.register_fake
+def _(x, scale=1.0, shift=0.0):
+    return torch.empty_like(x)
+
+
+@torch.library.custom_op("veles::saxpy", mutates_args=())
+def saxpy(a: float, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """a * x + y (fused multiply-add), returned as a new tensor."""
+    if not _gpu(x, "veles::saxpy"):
+        return torch.addcmul(y, x, torch.tensor(a, dtype=x.dtype))
+    x = x.contiguous()
+    out = y.contiguous().clone()
+    with on_device(x):
+        _lib.call("vs_saxpy", float(a), ptr(x), ptr(out), x.numel(), stream_of(x))
+    return out
+
+
+@saxpy.register_fake
+def _(a, x, y):
+    return torch.empty_like(y)
+
+
+# --------------------------------------------------------------------- math
+@torch.library.custom_op("veles::math", mutates_args=())
+def math(x: torch.Tensor, fn: str) -> torch.Tensor:
+    """sin / cos / log / exp (mathfun.h *_psv)."""
+    if not _gpu(x, "veles::math"):
+        return getattr(torch, fn)(x)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    with on_device(x):
+        _lib.call("vs_math", _FN[fn], ptr(x), ptr(out), x.numel(), stream_of(x))
+    return out
+
+
+@math.register_fake
+def _(x, fn):
+    return torch.empty_like(x)
+
+
+def sin(x):
+    return math(x, "sin")
+
+
+def cos(x):
+    return math(x, "cos")
+
+
+def log(x):
+    return math(x, "log")
+
+
+def exp(x):
+    return math(x, "exp")
+
+
+# --------------------------------------------------------------- reductions
+@torch.library.custom_op("veles::sum", mutates_args=())
+def sum_all(x: torch.Tensor) -> torch.Tensor:
+    """Sum of all elements as a 0-d tensor (sum_elements)."""
+    if not _gpu(x, "veles::sum"):
+        return x.sum()
+    x = x.contiguous()
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    with on_device(x):
+        _lib.call("vs_sum", ptr(x), x.numel(), ptr(out), stream_of(x))
+    return out
+
+
+@sum_all.register_fake
+def _(x):
+    return x.new_empty(())
+
+
+@torch.library.custom_op("veles::minmax", mutates_args=())
+def minmax(x: torch.Tensor) -> torch.Tensor:
+    """[min, max] of a float32 tensor (minmax1D) or a uint8 2-D plane
+    (minmax2D)."""
+    if x.dtype == torch.uint8:
+        if x.dim() != 2:
+            raise ValueError("veles::minmax: uint8 input must be 2-D")
+        if not _gpu(x, "veles::minmax"):
+            return torch.stack([x.min(), x.max()])
+        out = torch.empty(2, dtype=torch.uint8, device=x.device)
+        if x.stride(1) != 1:
+            x = x.contiguous()
+        with on_device(x):
+            _lib.call("vs_minmax2d_u8", ptr(x), x.stride(0), x.shape[1],
+                      x.shape[0], ptr(out), stream_of(x))
+        return out
+    if not _gpu(x, "veles::minmax"):
+        return torch.stack([x.min(), x.max()])
+    x = x.contiguous()
+    out = torch.empty(2, dtype=torch.float32, device=x.device)
+    with on_device(x):
+        _lib.call("vs_minmax", ptr(x), x.numel(), ptr(out), stream_of(x))
+    return out
+
+
+@minmax.register_fake
+def _(x):
+    return x.new_empty((2,))
+
+
+@torch.library.custom_op("veles::normalize2d", mutates_args=())
+def normalize2d(x: torch.Tensor) -> torch.Tensor:
+    """uint8 plane -> float32 in [-1, 1] (normalize2D), min/max found and
+    applied on the device without a host round trip."""
+    if x.dtype != torch.uint8 or x.dim() != 2:
+        raise ValueError("veles::normalize2d expects a 2-D uint8 tensor")
+    if not _gpu(x, "veles::normalize2d"):
+        mn, mx = int(x.min()), int(x.max())
+        if mn == mx:
+            return torch.zeros(x.shape, dtype=torch.float32)
+        return (x.float() - mn) / ((mx - mn) / 2.0) - 1.0
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    h, w = x.shape
+    out = torch.empty((h, w), dtype=torch.float32, device=x.device)
+    mm = torch.empty(2, dtype=torch.uint8, device=x.device)
+    with on_device(x):
+        s = stream_of(x)
+        _lib.call("vs_minmax2d_u8", ptr(x), x.stride(0), w, h, ptr(mm), s)
+        _lib.call("vs_normalize2d_u8", ptr(x), x.stride(0), w, h, ptr(mm), 0, 0,
+                  ptr(out), w, s)
+    return out
+
+
+@normalize2d.register_fake
+def _(x):
+    return torch.empty(x.shape, dtype=torch.float32, device=x.device)
