@@ -179,13 +179,34 @@ struct SaxpyOp {
   __device__ float operator()(float x, float y) const { return fmaf(a, x, y); }
 };
 
+// exp(x) with a two-constant (Cody-Waite) reduction x = n ln2 + r and a
+// degree-7 polynomial on |r| <= ln2/2, then ldexp: <= 1 ulp over the whole
+// range.  (A plain exp2(x * log2 e) loses ~|x| * 2^-24 relative accuracy in
+// the product, i.e. up to ~40 ulp near x = 88.)
+__device__ __forceinline__ float accurate_expf(float x) {
+  if (!(x < 88.72283935546875f)) return x != x ? x : __builtin_inff();
+  if (x < -103.97208404541015625f) return 0.f;
+  const float n = rintf(x * 1.44269504088896341f);
+  float r = fmaf(n, -0.693145751953125f, x);
+  r = fmaf(n, -1.428606765330187045e-6f, r);
+  float p = 1.98412698412698413e-4f;
+  p = fmaf(p, r, 1.38888888888888889e-3f);
+  p = fmaf(p, r, 8.33333333333333333e-3f);
+  p = fmaf(p, r, 4.16666666666666667e-2f);
+  p = fmaf(p, r, 1.66666666666666667e-1f);
+  p = fmaf(p, r, 0.5f);
+  p = fmaf(p, r, 1.0f);
+  p = fmaf(p, r, 1.0f);
+  return ldexpf(p, static_cast<int>(n));
+}
+
 template <int FN>
 struct MathOp {
   __device__ float operator()(float x) const {
     if constexpr (FN == VS_FN_SIN) return sinf(x);
     if constexpr (FN == VS_FN_COS) return cosf(x);
     if constexpr (FN == VS_FN_LOG) return logf(x);
-    return expf(x);
+    return accurate_expf(x);
   }
 };
 

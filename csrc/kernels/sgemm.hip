@@ -5,11 +5,11 @@
 // chain) that runs at the full fp32 vector rate while leaving the VALU free
 // for addressing and staging (cdna_hip_programming.md §3 'FP32-input MFMA').
 //
-// Structure (per workgroup, 256 threads = 4 waves):
-//   * output tile BM x BN = 128 x 128, each wave a 64 x 64 quadrant held as
-//     2 x 2 accumulators of 32 x 32 (64 accumulator registers);
-//   * K is walked in BK = 16 steps through two LDS buffers laid out k-major
-//     ([k][m], [k][n], rows padded to 132 floats), so an MFMA operand is one
+// Structure (template <BM, BN, BK, WM, WN>; WM x WN waves per workgroup):
+//   * each wave owns a (BM/WM) x (BN/WN) output block held as 32 x 32 MFMA
+//     accumulators (16 accumulator registers each);
+//   * K is walked in BK steps through two LDS buffers laid out k-major
+//     ([k][m], [k][n], rows padded by 4 floats), so an MFMA operand is one
 //     conflict-free ds_read_b32 per lane (32 consecutive floats per half-wave);
 //   * register-staged prefetch: the global loads of tile t+1 are issued before
 //     the MFMAs of tile t and written to the other LDS buffer after them
@@ -23,11 +23,12 @@
 //     (T1), and blockIdx.z walks the batch of strided-batched calls.
 //
 // Reference counterpart: src/matrix.c:200-252 (AVX dot-product GEMM with a
-// stack-copied B column, no blocking) and :53-65 / :67-80 (scalar).
+// stack-copied B column, no blocking) and :53-80 (scalar).
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "csrc/kernels/device.h"
 #include "csrc/runtime/runtime.h"
@@ -37,10 +38,6 @@ namespace vs {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int BM = 128, BN = 128, BK = 16;
-constexpr int kThreads = 256;
-constexpr int LDP = 132;  // LDS row pitch (floats): 128 + 4 keeps 16-B rows
 
 struct GemmArgs {
   int m, n, k;
@@ -53,131 +50,148 @@ struct GemmArgs {
   int64_t ldc, stride_c;
 };
 
-// Loads this thread's share of one BK x 128 operand tile into registers.
-//   KCONTIG: operand stored [mn][k] (k contiguous) -> 2 float4 along k.
-//   else   : operand stored [k][mn] (mn contiguous) -> 2 float4 along mn.
-template <bool KCONTIG, bool VEC>
-__device__ __forceinline__ void load_tile(const float *__restrict__ p,
-                                          int64_t ld, int mn0, int mn_lim,
-                                          int k0, int k_lim, float4 (&r)[2]) {
+template <int BM_, int BN_, int BK_, int WM_, int WN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int TM = BM / WM / 32;  // 32x32 tiles per wave along M
+  static constexpr int TN = BN / WN / 32;
+  static constexpr int PA = BM + 4;        // LDS pitch of the A tile (floats)
+  static constexpr int PB = BN + 4;
+  static constexpr int kLdsFloats = 2 * BK * (PA + PB);
+  static_assert(TM >= 1 && TN >= 1, "wave tile smaller than one MFMA tile");
+};
+
+// Loads this thread's share of one BK x BMN operand tile into registers.
+//   KCONTIG: operand stored [mn][k] (k contiguous) -> float4 along k.
+//   else   : operand stored [k][mn] (mn contiguous) -> float4 along mn.
+template <int BMN, int BK, int THREADS, bool KCONTIG, bool VEC>
+struct TileIO {
+  static constexpr int kLoads = BMN * BK / 4 / THREADS;
+  static_assert(kLoads * 4 * THREADS == BMN * BK, "tile not divisible");
+
+  __device__ static void load(const float *__restrict__ p, int64_t ld, int mn0,
+                             int mn_lim, int k0, int k_lim, float4 (&r)[kLoads]) {
 #pragma unroll
-  for (int l = 0; l < 2; l++) {
-    const int idx = threadIdx.x + l * kThreads;
-    int mn, kk;
-    if (KCONTIG) {
-      mn = mn0 + (idx >> 2);
-      kk = k0 + (idx & 3) * 4;
-    } else {
-      kk = k0 + (idx >> 5);
-      mn = mn0 + (idx & 31) * 4;
-    }
-    float v[4];
-    const float *base = KCONTIG ? p + mn * ld + kk : p + kk * ld + mn;
-    const bool full = KCONTIG ? (mn < mn_lim && kk + 3 < k_lim)
-                              : (kk < k_lim && mn + 3 < mn_lim);
-    if (VEC && full) {
-      const float4 t = *reinterpret_cast<const float4 *>(base);
-      v[0] = t.x;
-      v[1] = t.y;
-      v[2] = t.z;
-      v[3] = t.w;
-    } else {
+    for (int l = 0; l < kLoads; l++) {
+      const int idx = threadIdx.x + l * THREADS;
+      int mn, kk;
+      if (KCONTIG) {
+        mn = mn0 + idx / (BK / 4);
+        kk = k0 + (idx % (BK / 4)) * 4;
+      } else {
+        kk = k0 + idx / (BMN / 4);
+        mn = mn0 + (idx % (BMN / 4)) * 4;
+      }
+      const float *base = KCONTIG ? p + mn * ld + kk : p + kk * ld + mn;
+      const bool full = KCONTIG ? (mn < mn_lim && kk + 3 < k_lim)
+                                : (kk < k_lim && mn + 3 < mn_lim);
+      if (VEC && full) {
+        r[l] = *reinterpret_cast<const float4 *>(base);
+      } else {
+        float v[4];
 #pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const bool ok = KCONTIG ? (mn < mn_lim && kk + c < k_lim)
-                                : (kk < k_lim && mn + c < mn_lim);
-        v[c] = ok ? base[c] : 0.f;
+        for (int c = 0; c < 4; c++) {
+          const bool ok = KCONTIG ? (mn < mn_lim && kk + c < k_lim)
+                                  : (kk < k_lim && mn + c < mn_lim);
+          v[c] = ok ? base[c] : 0.f;
+        }
+        r[l] = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
-    r[l] = make_float4(v[0], v[1], v[2], v[3]);
   }
-}
 
-template <bool KCONTIG>
-__device__ __forceinline__ void store_tile(float *__restrict__ s,
-                                           const float4 (&r)[2]) {
+  __device__ static void store(float *__restrict__ s, int pitch,
+                              const float4 (&r)[kLoads]) {
 #pragma unroll
-  for (int l = 0; l < 2; l++) {
-    const int idx = threadIdx.x + l * kThreads;
-    if (KCONTIG) {
-      const int mn = idx >> 2, kq = (idx & 3) * 4;
-      s[(kq + 0) * LDP + mn] = r[l].x;
-      s[(kq + 1) * LDP + mn] = r[l].y;
-      s[(kq + 2) * LDP + mn] = r[l].z;
-      s[(kq + 3) * LDP + mn] = r[l].w;
-    } else {
-      const int kk = idx >> 5, mn = (idx & 31) * 4;
-      *reinterpret_cast<float4 *>(s + kk * LDP + mn) = r[l];
+    for (int l = 0; l < kLoads; l++) {
+      const int idx = threadIdx.x + l * THREADS;
+      if (KCONTIG) {
+        const int mn = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
+        s[(kq + 0) * pitch + mn] = r[l].x;
+        s[(kq + 1) * pitch + mn] = r[l].y;
+        s[(kq + 2) * pitch + mn] = r[l].z;
+        s[(kq + 3) * pitch + mn] = r[l].w;
+      } else {
+        const int kk = idx / (BMN / 4), mn = (idx % (BMN / 4)) * 4;
+        *reinterpret_cast<float4 *>(s + kk * pitch + mn) = r[l];
+      }
     }
   }
-}
+};
 
-// TA / TB: operand stored transposed relative to op().  A is KCONTIG unless
-// TA; B is KCONTIG only if TB.
-template <bool TA, bool TB, bool VEC>
-__global__ __launch_bounds__(kThreads) void sgemm_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float lds[2][2][BK * LDP];
+// TA / TB: operand stored transposed relative to op().  A is K-contiguous
+// unless TA; B is K-contiguous only if TB.
+template <class C, bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__(C::kThreads) void sgemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats];
+  using IOA = TileIO<C::BM, C::BK, C::kThreads, !TA, VEC>;
+  using IOB = TileIO<C::BN, C::BK, C::kThreads, TB, VEC>;
+  constexpr int BK = C::BK, PA = C::PA, PB = C::PB;
+  constexpr int kBuf = BK * (PA + PB);
 
-  const unsigned tiles_n = (g.n + BN - 1) / BN;
-  const unsigned tiles_m = (g.m + BM - 1) / BM;
-  const unsigned ntiles = tiles_m * tiles_n;
-  const unsigned t = dev::xcd_remap(blockIdx.x, ntiles);
-  const int tm = static_cast<int>(t / tiles_n), tn = static_cast<int>(t % tiles_n);
-  const int m0 = tm * BM, n0 = tn * BN;
+  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
+  const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
+  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = static_cast<int>(t / tiles_n) * C::BM;
+  const int n0 = static_cast<int>(t % tiles_n) * C::BN;
 
   const float *A = g.a + blockIdx.z * g.stride_a;
   const float *B = g.b + blockIdx.z * g.stride_b;
-  float *C = g.c + blockIdx.z * g.stride_c;
+  float *Cp = g.c + blockIdx.z * g.stride_c;
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / C::WN, wn = wid % C::WN;
   const int lrow = lane & 31, lk = lane >> 5;
+  const int am = wm * (C::BM / C::WM) + lrow;
+  const int bn = wn * (C::BN / C::WN) + lrow;
 
-  floatx16 acc[2][2];
+  floatx16 acc[C::TM][C::TN];
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < C::TM; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++)
+    for (int j = 0; j < C::TN; j++)
 #pragma unroll
       for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
 
-  float4 ra[2], rb[2];
+  float4 ra[IOA::kLoads], rb[IOB::kLoads];
   const int nk = (g.k + BK - 1) / BK;
 
-  load_tile<!TA, VEC>(A, g.lda, m0, g.m, 0, g.k, ra);
-  load_tile<TB, VEC>(B, g.ldb, n0, g.n, 0, g.k, rb);
-  store_tile<!TA>(lds[0][0], ra);
-  store_tile<TB>(lds[0][1], rb);
+  IOA::load(A, g.lda, m0, g.m, 0, g.k, ra);
+  IOB::load(B, g.ldb, n0, g.n, 0, g.k, rb);
+  IOA::store(lds, PA, ra);
+  IOB::store(lds + BK * PA, PB, rb);
   __syncthreads();
 
   for (int kt = 0; kt < nk; kt++) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      load_tile<!TA, VEC>(A, g.lda, m0, g.m, (kt + 1) * BK, g.k, ra);
-      load_tile<TB, VEC>(B, g.ldb, n0, g.n, (kt + 1) * BK, g.k, rb);
+      IOA::load(A, g.lda, m0, g.m, (kt + 1) * BK, g.k, ra);
+      IOB::load(B, g.ldb, n0, g.n, (kt + 1) * BK, g.k, rb);
     }
-    const float *As = lds[cur][0];
-    const float *Bs = lds[cur][1];
+    const float *As = lds + cur * kBuf;
+    const float *Bs = As + BK * PA;
 #pragma unroll
     for (int s = 0; s < BK / 2; s++) {
       const int kr = 2 * s + lk;
-      float fa[2], fb[2];
+      float fa[C::TM], fb[C::TN];
 #pragma unroll
-      for (int i = 0; i < 2; i++) fa[i] = As[kr * LDP + wm * 64 + i * 32 + lrow];
+      for (int i = 0; i < C::TM; i++) fa[i] = As[kr * PA + am + i * 32];
 #pragma unroll
-      for (int j = 0; j < 2; j++) fb[j] = Bs[kr * LDP + wn * 64 + j * 32 + lrow];
+      for (int j = 0; j < C::TN; j++) fb[j] = Bs[kr * PB + bn + j * 32];
 #pragma unroll
-      for (int i = 0; i < 2; i++)
+      for (int i = 0; i < C::TM; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < C::TN; j++)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j],
                                                            acc[i][j], 0, 0, 0);
     }
     if (more) {
-      store_tile<!TA>(lds[cur ^ 1][0], ra);
-      store_tile<TB>(lds[cur ^ 1][1], rb);
+      float *Ad = lds + (cur ^ 1) * kBuf;
+      IOA::store(Ad, PA, ra);
+      IOB::store(Ad + BK * PA, PB, rb);
     }
     __syncthreads();
   }
@@ -186,16 +200,16 @@ __global__ __launch_bounds__(kThreads) void sgemm_kernel(GemmArgs g) {
   // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
   const bool use_beta = g.beta != 0.f;
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < C::TM; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const int col = n0 + wn * 64 + j * 32 + lrow;
+    for (int j = 0; j < C::TN; j++) {
+      const int col = n0 + bn + j * 32;
       if (col >= g.n) continue;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int row = m0 + am - lrow + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
         if (row < g.m) {
-          float *pc = C + static_cast<int64_t>(row) * g.ldc + col;
+          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
           float v = g.alpha * acc[i][j][r];
           if (use_beta) v += g.beta * *pc;
           *pc = v;
@@ -204,18 +218,49 @@ __global__ __launch_bounds__(kThreads) void sgemm_kernel(GemmArgs g) {
     }
 }
 
-template <bool TA, bool TB>
-void launch_t(const GemmArgs &g, bool vec, dim3 grid, hipStream_t s) {
-  if (vec)
-    hipLaunchKernelGGL((sgemm_kernel<TA, TB, true>), grid, dim3(kThreads), 0, s, g);
-  else
-    hipLaunchKernelGGL((sgemm_kernel<TA, TB, false>), grid, dim3(kThreads), 0, s, g);
+template <class C>
+void launch_cfg(const GemmArgs &g, int ta, int tb, bool vec, int batch,
+                hipStream_t s) {
+  const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
+                                               ((g.n + C::BN - 1) / C::BN));
+  const dim3 grid(tiles, 1, static_cast<unsigned>(batch)), block(C::kThreads);
+#define VS_L(TA_, TB_)                                                       \
+  if (vec)                                                                   \
+    hipLaunchKernelGGL((sgemm_kernel<C, TA_, TB_, true>), grid, block, 0, s, g); \
+  else                                                                       \
+    hipLaunchKernelGGL((sgemm_kernel<C, TA_, TB_, false>), grid, block, 0, s, g);
+  if (!ta && !tb) {
+    VS_L(false, false)
+  } else if (!ta && tb) {
+    VS_L(false, true)
+  } else if (ta && !tb) {
+    VS_L(true, false)
+  } else {
+    VS_L(true, true)
+  }
+#undef VS_L
 }
 
-vs_status sgemm_impl(int ta, int tb, int m, int n, int k, float alpha,
-                     const float *a, int64_t lda, int64_t sa, const float *b,
-                     int64_t ldb, int64_t sb, float beta, float *c, int64_t ldc,
-                     int64_t sc, int batch, hipStream_t s) {
+// Tile variants (A/B-benchmarked on MI355X, see profiles/).
+using CfgSmall = Cfg<64, 64, 32, 2, 2>;     // small / skinny problems
+using CfgA = Cfg<128, 128, 16, 2, 2>;
+using CfgB = Cfg<128, 128, 32, 2, 2>;
+using CfgC = Cfg<256, 128, 16, 4, 2>;
+using CfgD = Cfg<128, 256, 16, 2, 4>;
+
+int default_variant() {
+  static const int v = [] {
+    const char *e = std::getenv("VELES_SGEMM_VARIANT");
+    return e && *e ? std::atoi(e) : -1;
+  }();
+  return v;
+}
+
+vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
+                     float alpha, const float *a, int64_t lda, int64_t sa,
+                     const float *b, int64_t ldb, int64_t sb, float beta,
+                     float *c, int64_t ldc, int64_t sc, int batch,
+                     hipStream_t s) {
   VS_REQUIRE(m >= 0 && n >= 0 && k >= 0 && batch >= 0,
              "vs_sgemm: negative dimension");
   if (m == 0 || n == 0 || batch == 0) return VS_OK;
@@ -230,13 +275,22 @@ vs_status sgemm_impl(int ta, int tb, int m, int n, int k, float alpha,
   };
   const bool vec = al(a) && al(b) && lda % 4 == 0 && ldb % 4 == 0 &&
                    (batch == 1 || (sa % 4 == 0 && sb % 4 == 0));
-  const unsigned tiles =
-      static_cast<unsigned>(((m + BM - 1) / BM) * ((n + BN - 1) / BN));
-  const dim3 grid(tiles, 1, static_cast<unsigned>(batch));
-  if (!ta && !tb) launch_t<false, false>(g, vec, grid, s);
-  else if (!ta && tb) launch_t<false, true>(g, vec, grid, s);
-  else if (ta && !tb) launch_t<true, false>(g, vec, grid, s);
-  else launch_t<true, true>(g, vec, grid, s);
+  if (variant < 0) variant = default_variant();
+  if (variant < 0) {
+    // Few 128x128 tiles cannot fill 256 CUs: use 64x64 tiles then.
+    const long tiles128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
+    variant = tiles128 < 256 ? 0 : 2;
+  }
+  switch (variant) {
+    case 0: launch_cfg<CfgSmall>(g, ta, tb, vec, batch, s); break;
+    case 1: launch_cfg<CfgA>(g, ta, tb, vec, batch, s); break;
+    case 2: launch_cfg<CfgB>(g, ta, tb, vec, batch, s); break;
+    case 3: launch_cfg<CfgC>(g, ta, tb, vec, batch, s); break;
+    case 4: launch_cfg<CfgD>(g, ta, tb, vec, batch, s); break;
+    default:
+      set_error("vs_sgemm: unknown variant %d", variant);
+      return VS_ERR_INVALID;
+  }
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
@@ -249,8 +303,8 @@ extern "C" {
 vs_status vs_sgemm(int ta, int tb, int m, int n, int k, float alpha,
                    const float *a, int64_t lda, const float *b, int64_t ldb,
                    float beta, float *c, int64_t ldc, vs_stream_t stream) {
-  return vs::sgemm_impl(ta, tb, m, n, k, alpha, a, lda, 0, b, ldb, 0, beta, c,
-                        ldc, 0, 1, static_cast<hipStream_t>(stream));
+  return vs::sgemm_impl(-1, ta, tb, m, n, k, alpha, a, lda, 0, b, ldb, 0, beta,
+                        c, ldc, 0, 1, static_cast<hipStream_t>(stream));
 }
 
 vs_status vs_sgemm_strided_batched(int ta, int tb, int m, int n, int k,
@@ -259,8 +313,17 @@ vs_status vs_sgemm_strided_batched(int ta, int tb, int m, int n, int k,
                                    int64_t sb, float beta, float *c,
                                    int64_t ldc, int64_t sc, int batch,
                                    vs_stream_t stream) {
-  return vs::sgemm_impl(ta, tb, m, n, k, alpha, a, lda, sa, b, ldb, sb, beta,
-                        c, ldc, sc, batch, static_cast<hipStream_t>(stream));
+  return vs::sgemm_impl(-1, ta, tb, m, n, k, alpha, a, lda, sa, b, ldb, sb,
+                        beta, c, ldc, sc, batch, static_cast<hipStream_t>(stream));
+}
+
+// Tuning entry point: run one explicit tile variant (0..4).
+vs_status vs_sgemm_variant(int variant, int ta, int tb, int m, int n, int k,
+                           float alpha, const float *a, int64_t lda,
+                           const float *b, int64_t ldb, float beta, float *c,
+                           int64_t ldc, vs_stream_t stream) {
+  return vs::sgemm_impl(variant, ta, tb, m, n, k, alpha, a, lda, 0, b, ldb, 0,
+                        beta, c, ldc, 0, 1, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

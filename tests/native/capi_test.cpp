@@ -109,6 +109,26 @@ TEST_CASE(normalize_golden) {
   }
 }
 
+TEST_CASE(normalize_pieces) {
+  std::vector<uint8_t> src(128 * 100, 1);
+  src[0] = 127;
+  src[10] = 252;
+  for (int simd = 0; simd < 2; simd++) {
+    uint8_t mn = 0, mx = 0;
+    minmax2D(simd, src.data(), 128, 100, 100, &mn, &mx);
+    CHECK_EQ(1, mn);
+    CHECK_EQ(252, mx);
+    std::vector<float> dst(100 * 100, 7.f);
+    normalize2D_minmax(simd, 1, 252, src.data(), 128, 100, 100, dst.data(), 100);
+    CHECK_NEAR(-1.f, dst[2], 1e-7);
+    CHECK_NEAR(1.f, dst[10], 1e-7);
+    if (dst[10] != 1.f)
+      std::printf("  simd=%d gpu=%d dst[0..3]=%g %g %g %g err='%s'\n", simd,
+                  vs_gpu_available(), dst[0], dst[1], dst[2], dst[3],
+                  vs_last_error());
+  }
+}
+
 TEST_CASE(mathfun_vs_double) {
   const int n = 199;
   float x[n], y[n];
@@ -119,8 +139,10 @@ TEST_CASE(mathfun_vs_double) {
       CHECK_NEAR(static_cast<float>(std::sin(double(x[i]))), y[i], 4e-7);
     exp_psv(simd, x, n, y);
     for (int i = 0; i < n; i++) {
-      const double e = std::exp(double(x[i]));
-      CHECK_NEAR(1.0, y[i] / e, 5e-7);
+      // ASSERT_FLOAT_EQ semantics: within 4 ulp of the rounded double result
+      const float e = static_cast<float>(std::exp(double(x[i])));
+      CHECK_NEAR(e, y[i], 4.0 * std::nextafter(std::fabs(e), INFINITY) -
+                              4.0 * std::fabs(e));
     }
   }
 }

@@ -7,6 +7,9 @@ import pytest
 
 from veles.simd_amd import capi
 
+# simd=1 is the GPU path: run it (gpu-marked) where a GPU exists.
+SIMDS = [0, pytest.param(1, marks=pytest.mark.gpu)]
+
 
 def _ulps(a, b):
     a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
@@ -16,7 +19,7 @@ def _ulps(a, b):
     return np.abs(a - b)
 
 
-@pytest.mark.parametrize("simd", [0, 1])
+@pytest.mark.parametrize("simd", SIMDS)
 @pytest.mark.parametrize("length", [1, 3, 64, 199, 100003])
 @pytest.mark.parametrize("name,ref", [("sin", math.sin), ("cos", math.cos),
                                       ("log", math.log), ("exp", math.exp)])

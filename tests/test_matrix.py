@@ -5,6 +5,9 @@ import pytest
 
 from veles.simd_amd import capi
 
+# simd=1 is the GPU path: run it (gpu-marked) where a GPU exists.
+SIMDS = [0, pytest.param(1, marks=pytest.mark.gpu)]
+
 
 def _fixture(w1, h1, w2, h2):
     # tests/matrix.cc:39-51: m1[i][j] = -j % 17 + i % 6, m2 = j % 15 - i % 5
@@ -33,7 +36,7 @@ def test_sub_validate():
 VALID = [1, -1, -5, 12, -12, -2, -22, 12]
 
 
-@pytest.mark.parametrize("simd", [0, 1])
+@pytest.mark.parametrize("simd", SIMDS)
 def test_multiply_validate(simd):
     m1 = [1, 2, 3, -2, 0, 4]
     m2 = [0, 1, 3, -2, 5, -1, 2, 4, -3, 0, -4, 2]
@@ -41,7 +44,7 @@ def test_multiply_validate(simd):
                                VALID, atol=0.01)
 
 
-@pytest.mark.parametrize("simd", [0, 1])
+@pytest.mark.parametrize("simd", SIMDS)
 def test_multiply_transposed_validate(simd):
     m1 = [1, 2, 3, -2, 0, 4]
     m2 = [0, 5, -3, 1, -1, 0, 3, 2, -4, -2, 4, 2]
@@ -54,6 +57,7 @@ SWEEP = ([(d, d, d, d) for d in (1, 3, 99)] +
          [(128, 300, 1000, 128), (125, 299, 999, 125)])
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("dims", SWEEP)
 @pytest.mark.parametrize("kind", ["add", "sub", "mul", "mulT"])
 def test_matrix_sweep(dims, kind):
@@ -78,6 +82,7 @@ def test_matrix_sweep(dims, kind):
     np.testing.assert_allclose(simd, base, atol=0.1)
 
 
+@pytest.mark.gpu
 def test_add_sub_125x299():
     m1, m2 = _fixture(125, 299, 125, 299)
     np.testing.assert_allclose(capi.matrix_add(1, m1, m2, 125, 299),

@@ -6,6 +6,9 @@ import pytest
 
 from veles.simd_amd import capi
 
+# simd=1 is the GPU path: run it (gpu-marked) where a GPU exists.
+SIMDS = [0, pytest.param(1, marks=pytest.mark.gpu)]
+
 
 def _plane():
     a = np.ones(128 * 100, np.uint8)
@@ -13,7 +16,7 @@ def _plane():
     return a
 
 
-@pytest.mark.parametrize("simd", [0, 1])
+@pytest.mark.parametrize("simd", SIMDS)
 def test_normalize2d(simd):
     src = _plane()
     res = np.zeros(100 * 100, np.float32)
@@ -26,7 +29,7 @@ def test_normalize2d(simd):
     np.testing.assert_allclose(res[121], f(2) * (3 - 1) / 251 - 1, rtol=1e-6)
 
 
-@pytest.mark.parametrize("simd", [0, 1])
+@pytest.mark.parametrize("simd", SIMDS)
 def test_minmax1d(simd):
     a = np.ones(100, np.float32)
     a[0], a[1], a[10], a[89], a[21] = 127, 15, 252, 31, 3
@@ -39,7 +42,7 @@ def test_minmax1d(simd):
     assert mx2.value == 252
 
 
-@pytest.mark.parametrize("simd", [0, 1])
+@pytest.mark.parametrize("simd", SIMDS)
 def test_minmax2d_and_flat(simd):
     src = _plane()
     mn, mx = ctypes.c_uint8(), ctypes.c_uint8()
