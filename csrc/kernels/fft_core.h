@@ -1,0 +1,234 @@
+// LDS-resident Stockham FFT building blocks for CDNA4.
+//
+// One signal of N = 2^LOGN complex points (N <= 16384) lives in LDS
+// (float2, one pad slot per 16 elements to break the power-of-two strides
+// of the early passes) while TPS = N/16 threads each own 16 points in
+// registers.  Each pass is a radix-R Stockham step (R in {2,4,8,16}):
+//   butterfly i in [0, N/R), k = i mod P (P = product of earlier radices):
+//     u_j = x[i + j N/R] * w^(j k),  w = exp(-+2 pi i / (P R))
+//     v   = DFT_R(u)
+//     y[(i - k) R + k + j P] = v_j
+// so the output is in natural order without a bit-reversal pass.  Inputs of
+// the first pass and outputs of the last pass are both "i + j N/R" with
+// consecutive i on consecutive lanes, i.e. coalesced global loads/stores, and
+// the last forward pass leaves in registers exactly the elements the first
+// pass of a reversed-radix inverse transform needs -- the fused convolution
+// kernels multiply by the filter spectrum in registers and start the inverse
+// FFT without an LDS round trip.
+//
+// Twiddles come from a per-size table exp(-2 pi i m / N), m < N, computed in
+// double precision on the host (csrc/kernels/fft_plan.h).
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace vs {
+namespace fft {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
+  return make_float2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ float2 csub(float2 a, float2 b) {
+  return make_float2(a.x - b.x, a.y - b.y);
+}
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a * conj(b)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+// z * (-i) forward, z * (+i) inverse
+template <bool INV>
+__device__ __forceinline__ float2 rot90(float2 z) {
+  return INV ? make_float2(-z.y, z.x) : make_float2(z.y, -z.x);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft2(float2 *v) {
+  const float2 a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(float2 &a0, float2 &a1, float2 &a2,
+                                     float2 &a3) {
+  const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+  const float2 t2 = cadd(a1, a3), t3 = rot90<INV>(csub(a1, a3));
+  a0 = cadd(t0, t2);
+  a2 = csub(t0, t2);
+  a1 = cadd(t1, t3);
+  a3 = csub(t1, t3);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(float2 *v) {
+  dft4<INV>(v[0], v[1], v[2], v[3]);
+}
+
+constexpr float kC8 = 0.70710678118654752440f;   // cos(pi/4)
+constexpr float kC16 = 0.92387953251128675613f;  // cos(pi/8)
+constexpr float kS16 = 0.38268343236508977173f;  // sin(pi/8)
+
+// z * exp(-+ i pi/4) and z * exp(-+ 3 i pi/4)
+template <bool INV>
+__device__ __forceinline__ float2 w8_1(float2 z) {
+  return INV ? make_float2(kC8 * (z.x - z.y), kC8 * (z.x + z.y))
+             : make_float2(kC8 * (z.x + z.y), kC8 * (z.y - z.x));
+}
+template <bool INV>
+__device__ __forceinline__ float2 w8_3(float2 z) {
+  return INV ? make_float2(-kC8 * (z.x + z.y), kC8 * (z.x - z.y))
+             : make_float2(kC8 * (z.y - z.x), -kC8 * (z.x + z.y));
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft8(float2 *v) {
+  float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+  float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+  dft4<INV>(e0, e1, e2, e3);
+  dft4<INV>(o0, o1, o2, o3);
+  o1 = w8_1<INV>(o1);
+  o2 = rot90<INV>(o2);
+  o3 = w8_3<INV>(o3);
+  v[0] = cadd(e0, o0);
+  v[4] = csub(e0, o0);
+  v[1] = cadd(e1, o1);
+  v[5] = csub(e1, o1);
+  v[2] = cadd(e2, o2);
+  v[6] = csub(e2, o2);
+  v[3] = cadd(e3, o3);
+  v[7] = csub(e3, o3);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft16(float2 *v) {
+  float2 e[8], o[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    e[j] = v[2 * j];
+    o[j] = v[2 * j + 1];
+  }
+  dft8<INV>(e);
+  dft8<INV>(o);
+  // o[k] *= exp(-+ 2 pi i k / 16)
+  const float sg = INV ? 1.f : -1.f;
+  o[1] = cmul(o[1], make_float2(kC16, sg * kS16));
+  o[2] = w8_1<INV>(o[2]);
+  o[3] = cmul(o[3], make_float2(kS16, sg * kC16));
+  o[4] = rot90<INV>(o[4]);
+  o[5] = cmul(o[5], make_float2(-kS16, sg * kC16));
+  o[6] = w8_3<INV>(o[6]);
+  o[7] = cmul(o[7], make_float2(-kC16, sg * kS16));
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    v[k] = cadd(e[k], o[k]);
+    v[k + 8] = csub(e[k], o[k]);
+  }
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void dft(float2 *v) {
+  if constexpr (R == 2) dft2<INV>(v);
+  else if constexpr (R == 4) dft4<INV>(v);
+  else if constexpr (R == 8) dft8<INV>(v);
+  else dft16<INV>(v);
+}
+
+// LDS index with one pad slot per 16 complex elements.
+__device__ __forceinline__ int pad(int e) { return e + (e >> 4); }
+
+// Compile-time pass plan for N = 2^LOGN, 16 points per thread (N >= 16).
+template <int LOGN_>
+struct Plan {
+  static constexpr int LOGN = LOGN_;
+  static constexpr int N = 1 << LOGN;
+  static constexpr int E = LOGN >= 4 ? 16 : N;     // points per thread
+  static constexpr int TPS = N / E;                // threads per signal
+  static constexpr int SMALL = LOGN >= 4 ? LOGN % 4 : 0;
+  static constexpr int NPASS = LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1;
+  static constexpr int kLds = N + N / 16 + 1;      // per-signal LDS (float2)
+  // Radix of pass q (forward order: the odd radix first).
+  static constexpr int radix(int q) {
+    return LOGN < 4 ? N : ((SMALL && q == 0) ? (1 << SMALL) : 16);
+  }
+  static constexpr int radix_rev(int q) { return radix(NPASS - 1 - q); }
+  static constexpr int stride(int q, bool rev) {
+    int p = 1;
+    for (int i = 0; i < q; i++) p *= rev ? radix_rev(i) : radix(i);
+    return p;
+  }
+  static constexpr int first_radix(bool rev) { return rev ? radix_rev(0) : radix(0); }
+  static constexpr int last_radix(bool rev) {
+    return rev ? radix_rev(NPASS - 1) : radix(NPASS - 1);
+  }
+};
+
+// Pass Q of a transform (REV: radices in reverse order).  On entry v holds
+// this pass's inputs (butterfly b: i = t + b TPS, v[b R + j] = x[i + j N/R]);
+// on exit from the last pass v holds the outputs in the same pattern.
+template <class PL, bool INV, bool REV, int Q>
+struct Pass {
+  static constexpr int R = REV ? PL::radix_rev(Q) : PL::radix(Q);
+  static constexpr int P = PL::stride(Q, REV);
+  static constexpr int NB = PL::E / R;
+
+  __device__ static void run(float2 (&v)[PL::E], float2 *lds, int t,
+                             const float2 *__restrict__ tw) {
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const int i = t + b * PL::TPS;
+      if constexpr (P > 1) {
+        const int k = i & (P - 1);
+        constexpr int S = PL::N / (P * R);
+#pragma unroll
+        for (int j = 1; j < R; j++) {
+          const float2 w = tw[j * k * S];
+          v[b * R + j] = INV ? cmulc(v[b * R + j], w) : cmul(v[b * R + j], w);
+        }
+      }
+      dft<R, INV>(&v[b * R]);
+    }
+    if constexpr (Q + 1 < PL::NPASS) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        const int i = t + b * PL::TPS;
+        const int k = i & (P - 1);
+        const int base = (i - k) * R + k;
+#pragma unroll
+        for (int j = 0; j < R; j++) lds[pad(base + j * P)] = v[b * R + j];
+      }
+      __syncthreads();
+      constexpr int R2 = REV ? PL::radix_rev(Q + 1) : PL::radix(Q + 1);
+#pragma unroll
+      for (int b = 0; b < PL::E / R2; b++) {
+        const int i = t + b * PL::TPS;
+#pragma unroll
+        for (int j = 0; j < R2; j++)
+          v[b * R2 + j] = lds[pad(i + j * (PL::N / R2))];
+      }
+      __syncthreads();
+      Pass<PL, INV, REV, Q + 1>::run(v, lds, t, tw);
+    }
+  }
+};
+
+// Element index held by v[b R + j] at the input of the first pass (FIRST)
+// or at the output of the last pass (R = that pass's radix).
+template <class PL, int R>
+__device__ __forceinline__ int reg_index(int t, int b, int j) {
+  return t + b * PL::TPS + j * (PL::N / R);
+}
+
+// Full transform: v (inputs of the first pass, pattern reg_index<first R>)
+// -> v (outputs of the last pass, pattern reg_index<last R>).
+template <class PL, bool INV, bool REV>
+__device__ __forceinline__ void transform(float2 (&v)[PL::E], float2 *lds,
+                                          int t, const float2 *__restrict__ tw) {
+  Pass<PL, INV, REV, 0>::run(v, lds, t, tw);
+}
+
+}  // namespace fft
+}  // namespace vs

@@ -278,8 +278,12 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
   if (variant < 0) variant = default_variant();
   if (variant < 0) {
     // Few 128x128 tiles cannot fill 256 CUs: use 64x64 tiles then.
-    const long tiles128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
-    variant = tiles128 < 256 ? 0 : 2;
+    // Largest tile that still gives every CU work (A/B on MI355X,
+    // profiles/r1/sgemm_variants.json): 128x256 when >= 512 tiles,
+    // 128x128 when >= 256, else 64x64.
+    const long t128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
+    const long t256 = static_cast<long>((m + 127) / 128) * ((n + 255) / 256) * batch;
+    variant = t256 >= 512 ? 4 : (t128 >= 256 ? 1 : 0);
   }
   switch (variant) {
     case 0: launch_cfg<CfgSmall>(g, ta, tb, vec, batch, s); break;

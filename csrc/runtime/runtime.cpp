@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -126,40 +127,139 @@ unsigned elementwise_grid(size_t work_items, unsigned block) {
   return static_cast<unsigned>(g);
 }
 
+static bool sync_stage() {
+  static const bool v = env_int("VELES_SYNC_STAGE", 0) != 0;
+  return v;
+}
+
+// Caching device allocator for library scratch and host staging.  Blocks are
+// tagged with the stream that last used them plus an event recorded at
+// release: the same stream reuses a block immediately (stream order makes it
+// safe), another stream only once the event has completed.  (The HIP
+// stream-ordered pool -- hipMallocAsync -- returned stale results on ROCm 7.2
+// after block reuse in our C API tests; this pool avoids depending on it.)
+class ScratchPool {
+ public:
+  static ScratchPool &get() {
+    static ScratchPool *pool = new ScratchPool();  // never destroyed
+    return *pool;
+  }
+
+  void *alloc(size_t bytes, hipStream_t stream) {
+    const size_t sz = round(bytes);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      for (auto it = free_.lower_bound(sz); it != free_.end(); ++it) {
+        if (it->first > 2 * sz + (1 << 20)) break;  // too wasteful
+        Block &b = it->second;
+        if (b.device != dev) continue;
+        if (b.stream != stream && hipEventQuery(b.event) != hipSuccess) continue;
+        void *p = b.ptr;
+        live_[p] = b;
+        free_.erase(it);
+        return p;
+      }
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, sz) != hipSuccess) {
+      (void)hipGetLastError();
+      release_all_free();  // retry once after dropping the cache
+      if (hipMalloc(&p, sz) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+    }
+    hipEvent_t ev = nullptr;
+    (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    std::lock_guard<std::mutex> lock(mu_);
+    live_[p] = Block{p, sz, dev, stream, ev};
+    return p;
+  }
+
+  void release(void *p, hipStream_t stream) {
+    std::lock_guard<std::mutex> lock(mu_);
+    auto it = live_.find(p);
+    if (it == live_.end()) return;
+    Block b = it->second;
+    live_.erase(it);
+    b.stream = stream;
+    (void)hipEventRecord(b.event, stream);
+    free_.emplace(b.size, b);
+  }
+
+  void release_all_free() {
+    std::lock_guard<std::mutex> lock(mu_);
+    for (auto &kv : free_) {
+      (void)hipEventSynchronize(kv.second.event);
+      (void)hipFree(kv.second.ptr);
+      (void)hipEventDestroy(kv.second.event);
+    }
+    free_.clear();
+  }
+
+ private:
+  struct Block {
+    void *ptr;
+    size_t size;
+    int device;
+    hipStream_t stream;
+    hipEvent_t event;
+  };
+  static size_t round(size_t b) {
+    if (b <= (1u << 20)) {
+      size_t s = 512;
+      while (s < b) s <<= 1;
+      return s;
+    }
+    const size_t g = 2u << 20;
+    return (b + g - 1) / g * g;
+  }
+  std::mutex mu_;
+  std::multimap<size_t, Block> free_;
+  std::map<void *, Block> live_;
+};
+
 vs_status DeviceBuffer::alloc(size_t bytes, hipStream_t stream) {
   release();
   stream_ = stream;
   bytes_ = bytes;
   if (bytes == 0) return VS_OK;
-  hipError_t e = hipMallocAsync(&ptr_, bytes, stream);
-  if (e != hipSuccess) {
-    ptr_ = nullptr;
+  ptr_ = ScratchPool::get().alloc(bytes, stream);
+  if (!ptr_) {
     bytes_ = 0;
-    set_error("hipMallocAsync(%zu bytes): %s", bytes, hipGetErrorString(e));
+    set_error("device allocation of %zu bytes failed", bytes);
     return VS_ERR_ALLOC;
   }
   return VS_OK;
 }
 
 void DeviceBuffer::release() {
-  if (ptr_) (void)hipFreeAsync(ptr_, stream_);
+  if (ptr_) ScratchPool::get().release(ptr_, stream_);
   ptr_ = nullptr;
   bytes_ = 0;
 }
+
+void release_cached_memory() { ScratchPool::get().release_all_free(); }
 
 Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)
     : user_(const_cast<void *>(user)), bytes_(bytes), dir_(dir),
       stream_(stream) {
   if (is_device_pointer(user)) {
     dev_ = user_;
+    log(2, "stage %p (%zu B): device pointer, used in place", user, bytes);
     return;
   }
+  log(2, "stage %p (%zu B): host buffer, dir=%d", user, bytes, static_cast<int>(dir));
   status_ = buf_.alloc(bytes, stream);
   if (status_ != VS_OK) return;
   dev_ = buf_.get();
   if ((dir & kIn) && bytes) {
     hipError_t e =
-        hipMemcpyAsync(dev_, user_, bytes, hipMemcpyHostToDevice, stream);
+        sync_stage()
+            ? hipMemcpyWithStream(dev_, user_, bytes, hipMemcpyHostToDevice, stream)
+            : hipMemcpyAsync(dev_, user_, bytes, hipMemcpyHostToDevice, stream);
     if (e != hipSuccess)
       status_ = hip_status(e, "stage-in hipMemcpyAsync", __FILE__, __LINE__);
   }
@@ -168,7 +268,10 @@ Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)
 vs_status Staged::finish() {
   if (status_ != VS_OK) return status_;
   if (dev_ == user_ || !(dir_ & kOut) || !bytes_) return VS_OK;
-  VS_HIP(hipMemcpyAsync(user_, dev_, bytes_, hipMemcpyDeviceToHost, stream_));
+  if (sync_stage())
+    VS_HIP(hipMemcpyWithStream(user_, dev_, bytes_, hipMemcpyDeviceToHost, stream_));
+  else
+    VS_HIP(hipMemcpyAsync(user_, dev_, bytes_, hipMemcpyDeviceToHost, stream_));
   return VS_OK;
 }
 
@@ -202,5 +305,6 @@ vs_status vs_stream_synchronize(vs_stream_t stream) {
   return VS_OK;
 }
 int vs_compiled_arch(void) { return 950; }
+void vs_release_cached_memory(void) { vs::release_cached_memory(); }
 
 }  // extern "C"

@@ -74,8 +74,8 @@ size_t gpu_min_elems();
 unsigned elementwise_grid(size_t work_items, unsigned block);
 
 // ------------------------------------------------------- scratch memory
-// Stream-ordered device allocation (hipMallocAsync); freed on destruction
-// with hipFreeAsync on the same stream.
+// Device scratch from the library's caching pool (stream-tagged blocks, see
+// runtime.cpp); returned to the pool, stream-ordered, on destruction.
 class DeviceBuffer {
  public:
   DeviceBuffer() = default;
@@ -107,6 +107,9 @@ class DeviceBuffer {
   size_t bytes_ = 0;
   hipStream_t stream_ = nullptr;
 };
+
+// Frees every cached (unused) pool block.
+void release_cached_memory();
 
 // ----------------------------------------------------------- staging
 // Presents a host-or-device operand as a device pointer on `stream`.

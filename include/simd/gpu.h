@@ -5,9 +5,10 @@
  *  Every vs_* compute function takes device pointers and a stream (a
  *  hipStream_t passed as void*; NULL is the HIP null stream) and is
  *  asynchronous with respect to the host: it only enqueues work.  Temporary
- *  device memory is taken from the stream-ordered pool (hipMallocAsync), so
- *  the calls are safe to use from several streams and to capture in graphs
- *  once their plans (FFT twiddles, filters) exist.
+ *  device memory comes from the library's caching pool (blocks tagged with the
+ *  stream that used them and an event), so the calls are safe to use from
+ *  several streams; after a warm-up call has populated the pool and the plans
+ *  (FFT twiddles), steady-state calls allocate nothing.
  *
  *  This is the layer the PyTorch custom ops (veles.simd_amd.ops) and the
  *  multi-GPU layer (veles.simd_amd.parallel) call; the source-compatible C
@@ -55,6 +56,8 @@ int vs_is_device_pointer(const void *ptr);
 vs_status vs_stream_synchronize(vs_stream_t stream);
 /// Number of the architecture the kernels were compiled for (950).
 int vs_compiled_arch(void);
+/// Returns the library's cached scratch memory to the device.
+void vs_release_cached_memory(void);
 
 /* ----------------------------------------------------------- elementwise */
 typedef enum { VS_OP_ADD = 0, VS_OP_SUB = 1, VS_OP_MUL = 2 } vs_binary_op;
@@ -120,6 +123,13 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
                                    int64_t stride_b, float beta, float *c,
                                    int64_t ldc, int64_t stride_c, int batch,
                                    vs_stream_t stream);
+
+/// Tuning entry point: one explicit SGEMM tile variant (0: 64x64x32,
+/// 1: 128x128x16, 2: 128x128x32, 3: 256x128x16, 4: 128x256x16).
+vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
+                           int k, float alpha, const float *a, int64_t lda,
+                           const float *b, int64_t ldb, float beta, float *c,
+                           int64_t ldc, vs_stream_t stream);
 
 /* ------------------------------------------------------------------- FFT */
 /// Unnormalised complex FFT of `batch` contiguous interleaved signals of n
