@@ -1,0 +1,278 @@
+// convolve.h / correlate.h (reference src/convolve.c, src/correlate.c).
+//
+// Handles keep the reference's by-value struct layout; their heap state is a
+// small plan record (fft_plan) describing the chosen GPU algorithm.  Operands
+// may be host or device pointers; host operands are staged through the
+// library stream and the call returns when the result is in place, like the
+// reference's synchronous API.  Without a GPU, the FFT / overlap-save handles
+// compute the same linear convolution with the host reference FFT.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include "simd/convolve.h"
+
+#include <cstdlib>
+#include <cstring>
+
+#include "csrc/api/dispatch.h"
+#include "csrc/ref/ref.h"
+#include "simd/correlate.h"
+#include "simd/gpu.h"
+
+using vs::Staged;
+
+namespace {
+
+struct ConvPlan {
+  int algorithm;  // vs_conv_algo actually executed
+  size_t x_length, h_length;
+  int block;      // transform length (informational)
+};
+
+int next_pow2_ge(size_t n) {
+  int p = 1;
+  while (static_cast<size_t>(p) < n) p <<= 1;
+  return p;
+}
+
+void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl,
+              const float *h, size_t hl, float *result) {
+  const size_t yl = xl + hl - 1;
+  vs::api::run_sync(what, [&](hipStream_t s) {
+    Staged y(result, yl * 4, Staged::kOut, s);
+    Staged xx(x, xl * 4, Staged::kIn, s), hh(h, hl * 4, Staged::kIn, s);
+    VS_TRY(y.status());
+    VS_TRY(xx.status());
+    VS_TRY(hh.status());
+    VS_TRY(vs_conv1d(algo, reverse, xx.dev<float>(), static_cast<int>(xl),
+                     static_cast<int64_t>(xl), hh.dev<float>(), static_cast<int>(hl),
+                     0, y.dev<float>(), static_cast<int64_t>(yl), 1, s));
+    return y.finish();
+  });
+}
+
+void run_plan(const char *what, ConvPlan *plan, int reverse, const float *x,
+              const float *h, float *result) {
+  if (!plan || !x || !h || !result) vs::fatal("%s: invalid arguments", what);
+  if (vs::gpu_available()) {
+    gpu_conv(what, plan->algorithm, reverse, x, plan->x_length, h, plan->h_length,
+             result);
+  } else {
+    vs::ref::convolve_fft(x, plan->x_length, h, plan->h_length, reverse, result);
+  }
+}
+
+ConvPlan *make_plan(int algo, size_t xl, size_t hl) {
+  if (xl == 0 || hl == 0) vs::fatal("convolution: empty input");
+  auto *p = static_cast<ConvPlan *>(std::malloc(sizeof(ConvPlan)));
+  p->algorithm = algo;
+  p->x_length = xl;
+  p->h_length = hl;
+  p->block = algo == VS_CONV_OVERLAP_SAVE
+                 ? vs_conv1d_os_block(static_cast<int>(hl))
+                 : next_pow2_ge(xl + hl - 1);
+  return p;
+}
+
+ConvolutionFFTHandle fft_init(size_t xl, size_t hl, int reverse) {
+  ConvolutionFFTHandle h;
+  std::memset(&h, 0, sizeof(h));
+  ConvPlan *p = make_plan(VS_CONV_FFT, xl, hl);
+  h.fft_plan = p;
+  h.fft_inverse_plan = p;
+  h.M = static_cast<int *>(std::malloc(sizeof(int)));
+  *h.M = p->block;
+  h.x_length = static_cast<int>(xl);
+  h.h_length = static_cast<int>(hl);
+  h.inputs = nullptr;
+  h.reverse = reverse;
+  return h;
+}
+
+void fft_fini(ConvolutionFFTHandle h) {
+  std::free(h.fft_plan);
+  std::free(h.M);
+}
+
+ConvolutionOverlapSaveHandle os_init(size_t xl, size_t hl, int reverse) {
+  // reference src/convolve.c:105: the filter must be shorter than half x.
+  if (!(hl < xl / 2) || hl == 0)
+    vs::fatal("overlap-save requires 0 < hLength < xLength / 2 (x=%zu h=%zu)", xl, hl);
+  ConvolutionOverlapSaveHandle h;
+  std::memset(&h, 0, sizeof(h));
+  ConvPlan *p = make_plan(VS_CONV_OVERLAP_SAVE, xl, hl);
+  h.fft_plan = p;
+  h.fft_inverse_plan = p;
+  h.x_length = xl;
+  h.h_length = hl;
+  h.L = static_cast<int *>(std::malloc(sizeof(int)));
+  *h.L = p->block;
+  h.reverse = reverse;
+  return h;
+}
+
+void os_fini(ConvolutionOverlapSaveHandle h) {
+  std::free(h.fft_plan);
+  std::free(h.L);
+}
+
+ConvolutionHandle auto_init(size_t xl, size_t hl, int reverse) {
+  ConvolutionHandle h;
+  std::memset(&h, 0, sizeof(h));
+  h.x_length = static_cast<int>(xl);
+  h.h_length = static_cast<int>(hl);
+  int algo;
+  if (vs::gpu_available()) {
+    algo = vs_conv1d_select(static_cast<int>(xl), static_cast<int>(hl), 1);
+    if (algo == VS_CONV_OVERLAP_SAVE && !(hl < xl / 2)) algo = VS_CONV_FFT;
+  } else {
+    // reference heuristic (src/convolve.c:349-363)
+    if (xl > hl * 2)
+      algo = xl > 200 ? VS_CONV_OVERLAP_SAVE : VS_CONV_DIRECT;
+    else
+      algo = xl > 350 ? VS_CONV_FFT : VS_CONV_DIRECT;
+  }
+  vs::log(1, "convolve_initialize(x=%zu, h=%zu): algorithm %d", xl, hl, algo);
+  switch (algo) {
+    case VS_CONV_OVERLAP_SAVE:
+      h.algorithm = kConvolutionAlgorithmOverlapSave;
+      h.handle.os = os_init(xl, hl, reverse);
+      break;
+    case VS_CONV_FFT:
+      h.algorithm = kConvolutionAlgorithmFFT;
+      h.handle.fft = fft_init(xl, hl, reverse);
+      break;
+    default:
+      h.algorithm = kConvolutionAlgorithmBruteForce;
+      break;
+  }
+  return h;
+}
+
+void direct(const char *what, int simd, int reverse, const float *x, size_t xl,
+            const float *h, size_t hl, float *result) {
+  if (!x || !h || !result || !xl || !hl) vs::fatal("%s: invalid arguments", what);
+  if (vs::api::use_gpu_simd(simd, what)) {
+    gpu_conv(what, VS_CONV_DIRECT, reverse, x, xl, h, hl, result);
+  } else if (reverse) {
+    vs::ref::correlate_direct(x, xl, h, hl, result);
+  } else {
+    vs::ref::convolve_direct(x, xl, h, hl, result);
+  }
+}
+
+void auto_run(ConvolutionHandle handle, const float *x, const float *h,
+              float *result, int reverse) {
+  switch (handle.algorithm) {
+    case kConvolutionAlgorithmFFT:
+      run_plan("convolve_fft", static_cast<ConvPlan *>(handle.handle.fft.fft_plan),
+               handle.handle.fft.reverse, x, h, result);
+      break;
+    case kConvolutionAlgorithmOverlapSave:
+      run_plan("convolve_overlap_save",
+               static_cast<ConvPlan *>(handle.handle.os.fft_plan),
+               handle.handle.os.reverse, x, h, result);
+      break;
+    case kConvolutionAlgorithmBruteForce:
+      direct(reverse ? "cross_correlate" : "convolve", 1, reverse, x,
+             handle.x_length, h, handle.h_length, result);
+      break;
+  }
+}
+
+void auto_fini(ConvolutionHandle handle) {
+  switch (handle.algorithm) {
+    case kConvolutionAlgorithmFFT:
+      fft_fini(handle.handle.fft);
+      break;
+    case kConvolutionAlgorithmOverlapSave:
+      os_fini(handle.handle.os);
+      break;
+    case kConvolutionAlgorithmBruteForce:
+      break;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+/* ------------------------------------------------------------ convolve */
+ConvolutionFFTHandle convolve_fft_initialize(size_t xl, size_t hl) {
+  return fft_init(xl, hl, 0);
+}
+void convolve_fft(ConvolutionFFTHandle handle, const float *x, const float *h,
+                  float *result) {
+  run_plan("convolve_fft", static_cast<ConvPlan *>(handle.fft_plan), handle.reverse,
+           x, h, result);
+}
+void convolve_fft_finalize(ConvolutionFFTHandle handle) { fft_fini(handle); }
+
+ConvolutionOverlapSaveHandle convolve_overlap_save_initialize(size_t xl,
+                                                              size_t hl) {
+  return os_init(xl, hl, 0);
+}
+void convolve_overlap_save(ConvolutionOverlapSaveHandle handle, const float *x,
+                           const float *h, float *result) {
+  run_plan("convolve_overlap_save", static_cast<ConvPlan *>(handle.fft_plan),
+           handle.reverse, x, h, result);
+}
+void convolve_overlap_save_finalize(ConvolutionOverlapSaveHandle handle) {
+  os_fini(handle);
+}
+
+void convolve_simd(int simd, const float *x, size_t xl, const float *h,
+                   size_t hl, float *result) {
+  direct("convolve_simd", simd, 0, x, xl, h, hl, result);
+}
+
+ConvolutionHandle convolve_initialize(size_t xl, size_t hl) {
+  return auto_init(xl, hl, 0);
+}
+void convolve(ConvolutionHandle handle, const float *x, const float *h,
+              float *result) {
+  auto_run(handle, x, h, result, 0);
+}
+void convolve_finalize(ConvolutionHandle handle) { auto_fini(handle); }
+
+/* ----------------------------------------------------------- correlate */
+CrossCorrelationFFTHandle cross_correlate_fft_initialize(size_t xl, size_t hl) {
+  return fft_init(xl, hl, 1);
+}
+void cross_correlate_fft(CrossCorrelationFFTHandle handle, const float *x,
+                         const float *h, float *result) {
+  convolve_fft(handle, x, h, result);
+}
+void cross_correlate_fft_finalize(CrossCorrelationFFTHandle handle) {
+  fft_fini(handle);
+}
+
+CrossCorrelationOverlapSaveHandle cross_correlate_overlap_save_initialize(
+    size_t xl, size_t hl) {
+  return os_init(xl, hl, 1);
+}
+void cross_correlate_overlap_save(CrossCorrelationOverlapSaveHandle handle,
+                                  const float *x, const float *h,
+                                  float *result) {
+  convolve_overlap_save(handle, x, h, result);
+}
+void cross_correlate_overlap_save_finalize(
+    CrossCorrelationOverlapSaveHandle handle) {
+  os_fini(handle);
+}
+
+void cross_correlate_simd(int simd, const float *x, size_t xl, const float *h,
+                          size_t hl, float *result) {
+  direct("cross_correlate_simd", simd, 1, x, xl, h, hl, result);
+}
+
+CrossCorrelationHandle cross_correlate_initialize(size_t xl, size_t hl) {
+  return auto_init(xl, hl, 1);
+}
+void cross_correlate(CrossCorrelationHandle handle, const float *x,
+                     const float *h, float *result) {
+  auto_run(handle, x, h, result, 1);
+}
+void cross_correlate_finalize(CrossCorrelationHandle handle) {
+  auto_fini(handle);
+}
+
+}  // extern "C"

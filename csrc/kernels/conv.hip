@@ -1,0 +1,453 @@
+// Batched 1D convolution / cross-correlation.
+//
+// Three algorithms, as in the reference (src/convolve.c), all on the GPU:
+//   * direct: LDS-tiled brute force.  A 256-thread block produces 2048
+//     consecutive outputs; the filter is walked in 512-tap chunks staged in
+//     LDS together with the matching x window (one pad word per 32 so the
+//     8-outputs-per-lane sliding window reads are bank-conflict free); each
+//     lane keeps a 15-sample register window, i.e. 2 LDS reads per 8 FMAs.
+//   * overlap-save: ONE fused kernel for all blocks of all signals.  A
+//     workgroup takes two blocks (the first in the real part, the second in
+//     the imaginary part of one complex L-point FFT -- valid because the
+//     filter is real), transforms them in LDS, multiplies by the filter
+//     spectrum in registers, runs the inverse transform with the radix order
+//     reversed (no LDS round trip in between, fft_core.h) and writes the
+//     `step` valid samples of each block.  The reference runs this block loop
+//     serially through FFTF (src/convolve.c:181-228).
+//   * FFT: the same fused kernel with a single block per signal when the
+//     padded length fits one workgroup (<= 16384); beyond that a four-step
+//     transform through HBM (fft.hip) with the spectra multiplied in place.
+// Correlation is convolution with the filter reversed at upload
+// (src/convolve.c:167-171, :302-306), except in the direct kernel which reads
+// the taps reversed.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "csrc/kernels/device.h"
+#include "csrc/kernels/fft_core.h"
+#include "csrc/kernels/fft_plan.h"
+#include "csrc/runtime/runtime.h"
+#include "simd/gpu.h"
+
+namespace vs {
+namespace conv {
+namespace {
+
+using fft::cmul;
+using fft::Plan;
+using fft::reg_index;
+
+// ------------------------------------------------------------- direct
+constexpr int kDirThreads = 256;
+constexpr int kDirPerThread = 8;
+constexpr int kDirOut = kDirThreads * kDirPerThread;  // outputs per block
+constexpr int kDirTaps = 512;                          // taps per LDS chunk
+constexpr int kDirX = kDirOut + kDirTaps;              // x window (+1 spare)
+
+__device__ __forceinline__ int xpad(int i) { return i + (i >> 5); }
+
+__global__ __launch_bounds__(kDirThreads) void direct_kernel(
+    const float *__restrict__ x, int xlen, int64_t xs, const float *__restrict__ h,
+    int hlen, int64_t hs, float *__restrict__ y, int64_t ys, int ylen,
+    int reverse) {
+  __shared__ float sx[kDirX + kDirX / 32 + 1];
+  __shared__ float sh[kDirTaps];
+  const int sig = blockIdx.y;
+  const float *xrow = x + sig * xs;
+  const float *hrow = h + sig * hs;
+  const int n0 = blockIdx.x * kDirOut;
+  const int q0 = threadIdx.x * kDirPerThread;
+  float acc[kDirPerThread];
+#pragma unroll
+  for (int r = 0; r < kDirPerThread; r++) acc[r] = 0.f;
+
+  for (int m0 = 0; m0 < hlen; m0 += kDirTaps) {
+    const int taps = min(kDirTaps, hlen - m0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kDirTaps; i += kDirThreads) {
+      float v = 0.f;
+      if (i < taps) v = reverse ? hrow[hlen - 1 - (m0 + i)] : hrow[m0 + i];
+      sh[i] = v;
+    }
+    // x window: xw[i] = x[n0 - m0 - kDirTaps + i], i < kDirX
+    const int xbase = n0 - m0 - kDirTaps;
+    for (int i = threadIdx.x; i < kDirX; i += kDirThreads) {
+      const int p = xbase + i;
+      sx[xpad(i)] = (p >= 0 && p < xlen) ? xrow[p] : 0.f;
+    }
+    __syncthreads();
+    // y[n0 + q0 + r] += sum_mm sh[mm] * xw[q0 + r - mm + kDirTaps]
+    float w[2 * kDirPerThread];
+    const int top = q0 + kDirTaps;
+#pragma unroll
+    for (int r = 0; r < kDirPerThread; r++) w[kDirPerThread + r] = sx[xpad(top + r)];
+    for (int mm = 0; mm < kDirTaps; mm += kDirPerThread) {
+#pragma unroll
+      for (int r = 0; r < kDirPerThread; r++)
+        w[r] = sx[xpad(top - mm - kDirPerThread + r)];
+#pragma unroll
+      for (int u = 0; u < kDirPerThread; u++) {
+        const float hv = sh[mm + u];
+#pragma unroll
+        for (int r = 0; r < kDirPerThread; r++)
+          acc[r] = fmaf(hv, w[kDirPerThread + r - u], acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < kDirPerThread; r++) w[kDirPerThread + r] = w[r];
+    }
+  }
+  float *yrow = y + sig * ys;
+#pragma unroll
+  for (int r = 0; r < kDirPerThread; r++) {
+    const int n = n0 + q0 + r;
+    if (n < ylen) yrow[n] = acc[r];
+  }
+}
+
+// ------------------------------------------------------ filter spectrum
+// hc[f][n] = (reversed?) h[f][n] + 0i for n < hlen, 0 beyond (length L).
+__global__ __launch_bounds__(256) void pad_filter_kernel(
+    const float *__restrict__ h, int hlen, int64_t hs, int reverse, int logl,
+    int nfilt, float2 *__restrict__ hc) {
+  const long long L = 1LL << logl;
+  const long long total = L * nfilt;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total;
+       g += static_cast<long long>(gridDim.x) * 256) {
+    const long long f = g >> logl;
+    const int n = static_cast<int>(g & (L - 1));
+    float v = 0.f;
+    if (n < hlen) v = h[f * hs + (reverse ? hlen - 1 - n : n)];
+    hc[g] = make_float2(v, 0.f);
+  }
+}
+
+// ------------------------------------------------ fused block convolution
+struct BlockArgs {
+  const float *x;
+  int64_t xs;
+  int xlen;
+  float *y;
+  int64_t ys;
+  int ylen;
+  const float2 *H;  // spectrum, natural order, L per filter
+  int h_per_signal;
+  int pre;    // history samples per block (h_len - 1 for overlap-save)
+  int step;   // valid outputs per block
+  int nblk;   // block slots per signal (even when filters are per signal)
+  long long nslots;
+  float scale;
+};
+
+template <int LOGN>
+__global__ __launch_bounds__(Plan<LOGN>::TPS) void block_conv_kernel(
+    BlockArgs a, const float2 *__restrict__ tw) {
+  using PL = Plan<LOGN>;
+  __shared__ float2 lds[PL::kLds];
+  const int t = threadIdx.x;
+  const long long s0 = 2LL * blockIdx.x, s1 = s0 + 1;
+  const long long sig0 = s0 / a.nblk, sig1 = s1 / a.nblk;
+  const int b0 = static_cast<int>(s0 % a.nblk), b1 = static_cast<int>(s1 % a.nblk);
+  const bool ok0 = b0 * static_cast<long long>(a.step) < a.ylen;
+  const bool ok1 = s1 < a.nslots && b1 * static_cast<long long>(a.step) < a.ylen;
+  const float *x0 = a.x + sig0 * a.xs;
+  const float *x1 = a.x + sig1 * a.xs;
+  const int st0 = b0 * a.step - a.pre, st1 = b1 * a.step - a.pre;
+
+  float2 v[PL::E];
+  constexpr int R0 = PL::first_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+    for (int j = 0; j < R0; j++) {
+      const int n = reg_index<PL, R0>(t, b, j);
+      const int p0 = st0 + n, p1 = st1 + n;
+      v[b * R0 + j] =
+          make_float2(ok0 && p0 >= 0 && p0 < a.xlen ? x0[p0] : 0.f,
+                      ok1 && p1 >= 0 && p1 < a.xlen ? x1[p1] : 0.f);
+    }
+  fft::transform<PL, false, false>(v, lds, t, tw);
+
+  // Multiply by the filter spectrum (both slots share it).
+  const float2 *H = a.H + (a.h_per_signal ? sig0 * PL::N : 0);
+  constexpr int RL = PL::last_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++)
+      v[b * RL + j] = cmul(v[b * RL + j], H[reg_index<PL, RL>(t, b, j)]);
+
+  __syncthreads();  // LDS reuse by the inverse transform
+  fft::transform<PL, true, true>(v, lds, t, tw);
+
+  constexpr int RI = PL::radix(0);  // last radix of the reversed plan
+  float *y0 = a.y + sig0 * a.ys;
+  float *y1 = a.y + sig1 * a.ys;
+#pragma unroll
+  for (int b = 0; b < PL::E / RI; b++)
+#pragma unroll
+    for (int j = 0; j < RI; j++) {
+      const int n = reg_index<PL, RI>(t, b, j) - a.pre;
+      if (n < 0 || n >= a.step) continue;
+      const float2 r = v[b * RI + j];
+      const long long o0 = static_cast<long long>(b0) * a.step + n;
+      const long long o1 = static_cast<long long>(b1) * a.step + n;
+      if (ok0 && o0 < a.ylen) y0[o0] = r.x * a.scale;
+      if (ok1 && o1 < a.ylen) y1[o1] = r.y * a.scale;
+    }
+}
+
+template <int LOGN>
+void launch_block_t(const BlockArgs &a, const float2 *tw, hipStream_t s) {
+  const unsigned grid = static_cast<unsigned>((a.nslots + 1) / 2);
+  hipLaunchKernelGGL((block_conv_kernel<LOGN>), dim3(grid), dim3(Plan<LOGN>::TPS),
+                     0, s, a, tw);
+}
+
+// ------------------------------------------ large FFT path (four-step)
+// z[p][n] = x[2p][n] + i x[2p+1][n] (zero padded to 2^logm)
+__global__ __launch_bounds__(256) void pack_pairs_kernel(
+    const float *__restrict__ x, int xlen, int64_t xs, int batch, int logm,
+    long long npairs, float2 *__restrict__ z) {
+  const long long M = 1LL << logm;
+  const long long total = npairs * M;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total;
+       g += static_cast<long long>(gridDim.x) * 256) {
+    const long long p = g >> logm;
+    const int n = static_cast<int>(g & (M - 1));
+    const long long s0 = 2 * p, s1 = 2 * p + 1;
+    const float a = n < xlen ? x[s0 * xs + n] : 0.f;
+    const float b = (n < xlen && s1 < batch) ? x[s1 * xs + n] : 0.f;
+    z[g] = make_float2(a, b);
+  }
+}
+
+__global__ __launch_bounds__(256) void unpack_pairs_kernel(
+    const float2 *__restrict__ z, int logm, long long npairs, int batch,
+    float *__restrict__ y, int64_t ys, int ylen, float scale) {
+  const long long M = 1LL << logm;
+  const long long total = npairs * ylen;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total;
+       g += static_cast<long long>(gridDim.x) * 256) {
+    const long long p = g / ylen;
+    const int n = static_cast<int>(g % ylen);
+    const float2 v = z[p * M + n];
+    y[2 * p * ys + n] = v.x * scale;
+    if (2 * p + 1 < batch) y[(2 * p + 1) * ys + n] = v.y * scale;
+  }
+}
+
+// z[p] *= H[p or 0] over the four-step (permuted) spectrum layout
+__global__ __launch_bounds__(256) void spectrum_mul_kernel(
+    float2 *__restrict__ z, const float2 *__restrict__ H, int logm,
+    long long npairs, int h_per_pair) {
+  const long long M = 1LL << logm;
+  const long long total = npairs * M;
+  for (long long g = blockIdx.x * 256LL + threadIdx.x; g < total;
+       g += static_cast<long long>(gridDim.x) * 256) {
+    const long long hi = h_per_pair ? g : (g & (M - 1));
+    z[g] = cmul(z[g], H[hi]);
+  }
+}
+
+}  // namespace
+
+int os_block_log(int hlen) {
+  // Reference block size 2^(floor(log2 M) + 2) (src/convolve.c:116-121),
+  // raised to >= 2048 so every block amortises its transform over >= ~75%
+  // useful outputs, capped at the single-workgroup LDS transform.
+  int lg = 2;
+  int m = hlen;
+  while (m >>= 1) lg++;
+  if (lg < 11) lg = 11;
+  if (lg > fft::kMaxLdsLog) lg = fft::kMaxLdsLog;
+  return lg;
+}
+
+int select(int xlen, int hlen, int batch) {
+  const long long ylen = static_cast<long long>(xlen) + hlen - 1;
+  (void)batch;
+  if (hlen <= 32 || ylen <= 64) return VS_CONV_DIRECT;
+  const int los = os_block_log(hlen);
+  const bool os_ok = (1 << los) - (hlen - 1) >= (1 << los) / 2;  // >= 50% useful
+  int lm = 1;
+  while ((1LL << lm) < ylen) lm++;
+  if (lm <= fft::kMaxLdsLog && (!os_ok || ylen <= (1LL << los)))
+    return VS_CONV_FFT;  // one block covers the whole output
+  if (os_ok) return VS_CONV_OVERLAP_SAVE;
+  return VS_CONV_FFT;
+}
+
+vs_status run_direct(int correlate, const float *x, int xlen, int64_t xs,
+                     const float *h, int hlen, int64_t hs, float *y, int64_t ys,
+                     int batch, hipStream_t s) {
+  const int ylen = xlen + hlen - 1;
+  const dim3 grid(static_cast<unsigned>((ylen + kDirOut - 1) / kDirOut),
+                  static_cast<unsigned>(batch));
+  hipLaunchKernelGGL(direct_kernel, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
+                     hlen, hs, y, ys, ylen, correlate);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+// Spectra (natural order, 2^logl points) of the nfilt filters.
+vs_status filter_spectra(int correlate, const float *h, int hlen, int64_t hs,
+                         int nfilt, int logl, DeviceBuffer &out, hipStream_t s) {
+  const size_t n = (static_cast<size_t>(1) << logl) * nfilt;
+  VS_TRY(out.alloc(n * sizeof(float2), s));
+  hipLaunchKernelGGL(pad_filter_kernel, dim3(elementwise_grid(n, 256)), dim3(256), 0,
+                     s, h, hlen, hs, correlate, logl, nfilt, out.as<float2>());
+  VS_HIP(hipGetLastError());
+  return fft::launch_c2c_lds(logl, false, out.as<float2>(), out.as<float2>(), nfilt, s);
+}
+
+vs_status run_block(int correlate, bool overlap_save, const float *x, int xlen,
+                    int64_t xs, const float *h, int hlen, int64_t hs, float *y,
+                    int64_t ys, int batch, hipStream_t s) {
+  const int ylen = xlen + hlen - 1;
+  int logl;
+  if (overlap_save) {
+    logl = os_block_log(hlen);
+  } else {
+    logl = 4;  // smallest instantiated transform
+    while ((1 << logl) < ylen) logl++;
+  }
+  VS_REQUIRE(logl <= fft::kMaxLdsLog, "block convolution: block 2^%d too large", logl);
+  const int L = 1 << logl;
+  BlockArgs a{};
+  a.x = x;
+  a.xs = xs;
+  a.xlen = xlen;
+  a.y = y;
+  a.ys = ys;
+  a.ylen = ylen;
+  a.pre = overlap_save ? hlen - 1 : 0;
+  a.step = L - a.pre;
+  VS_REQUIRE(a.step > 0, "overlap-save: filter (%d) longer than the block (%d)", hlen, L);
+  a.nblk = (ylen + a.step - 1) / a.step;
+  a.h_per_signal = hs != 0;
+  if (a.h_per_signal && (a.nblk & 1)) a.nblk++;  // never pair across filters
+  a.nslots = static_cast<long long>(a.nblk) * batch;
+  a.scale = 1.0f / static_cast<float>(L);
+  DeviceBuffer spec;
+  VS_TRY(filter_spectra(correlate, h, hlen, hs, a.h_per_signal ? batch : 1, logl,
+                        spec, s));
+  a.H = spec.as<float2>();
+  vs_status st;
+  const float2 *tw = fft::twiddles(logl, &st);
+  if (!tw) return st;
+  switch (logl) {
+#define VS_CASE(LG) \
+  case LG: launch_block_t<LG>(a, tw, s); break;
+    VS_CASE(4) VS_CASE(5) VS_CASE(6) VS_CASE(7) VS_CASE(8) VS_CASE(9)
+    VS_CASE(10) VS_CASE(11) VS_CASE(12) VS_CASE(13) VS_CASE(14)
+#undef VS_CASE
+    default:
+      set_error("block convolution: unsupported block 2^%d", logl);
+      return VS_ERR_UNSUPPORTED;
+  }
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status run_fft_large(int correlate, const float *x, int xlen, int64_t xs,
+                        const float *h, int hlen, int64_t hs, float *y, int64_t ys,
+                        int batch, hipStream_t s) {
+  const int ylen = xlen + hlen - 1;
+  int logm = 1;
+  while ((1LL << logm) < ylen) logm++;
+  VS_REQUIRE(logm <= fft::kMaxLog, "FFT convolution: padded length 2^%d too large",
+             logm);
+  int log1, log2;
+  fft::four_step_split(logm, &log1, &log2);
+  const long long M = 1LL << logm;
+  const long long npairs = (batch + 1) / 2;
+  const bool per = hs != 0;
+  // Filters: a complex signal per pair of outputs when filters differ; the
+  // two members of a pair use different filters then, so fall back to one
+  // signal per transform (imaginary part zero) in that case.
+  if (per) {
+    for (int b = 0; b < batch; b++) {
+      VS_TRY(run_fft_large(correlate, x + b * xs, xlen, 0, h + b * hs, hlen, 0,
+                           y + b * ys, ylen, 1, s));
+    }
+    return VS_OK;
+  }
+  DeviceBuffer hz, z;
+  VS_TRY(hz.alloc(M * sizeof(float2), s));
+  VS_TRY(z.alloc(M * npairs * sizeof(float2), s));
+  hipLaunchKernelGGL(pad_filter_kernel, dim3(elementwise_grid(M, 256)), dim3(256), 0,
+                     s, h, hlen, hs, correlate, logm, 1, hz.as<float2>());
+  VS_TRY(fft::launch_cols(logm, false, hz.as<float2>(), hz.as<float2>(), 1, s));
+  VS_TRY(fft::launch_c2c_lds(log2, false, hz.as<float2>(), hz.as<float2>(), 1 << log1, s));
+  hipLaunchKernelGGL(pack_pairs_kernel, dim3(elementwise_grid(M * npairs, 256)),
+                     dim3(256), 0, s, x, xlen, xs, batch, logm, npairs, z.as<float2>());
+  VS_TRY(fft::launch_cols(logm, false, z.as<float2>(), z.as<float2>(), npairs, s));
+  VS_TRY(fft::launch_c2c_lds(log2, false, z.as<float2>(), z.as<float2>(),
+                             static_cast<int>(npairs << log1), s));
+  hipLaunchKernelGGL(spectrum_mul_kernel, dim3(elementwise_grid(M * npairs, 256)),
+                     dim3(256), 0, s, z.as<float2>(), hz.as<float2>(), logm, npairs, 0);
+  VS_TRY(fft::launch_c2c_lds(log2, true, z.as<float2>(), z.as<float2>(),
+                             static_cast<int>(npairs << log1), s));
+  VS_TRY(fft::launch_cols(logm, true, z.as<float2>(), z.as<float2>(), npairs, s));
+  hipLaunchKernelGGL(unpack_pairs_kernel, dim3(elementwise_grid(npairs * ylen, 256)),
+                     dim3(256), 0, s, z.as<float2>(), logm, npairs, batch, y, ys, ylen,
+                     1.0f / static_cast<float>(M));
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+}  // namespace conv
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" {
+
+int vs_conv1d_select(int xlen, int hlen, int batch) {
+  return conv::select(xlen, hlen, batch);
+}
+
+int vs_conv1d_os_block(int hlen) { return 1 << conv::os_block_log(hlen); }
+
+vs_status vs_conv1d(int algo, int correlate, const float *x, int xlen,
+                    int64_t xs, const float *h, int hlen, int64_t hs, float *y,
+                    int64_t ys, int batch, vs_stream_t stream) {
+  VS_REQUIRE(x && h && y, "vs_conv1d: null pointer");
+  VS_REQUIRE(xlen > 0 && hlen > 0 && batch >= 0, "vs_conv1d: empty input");
+  const long long ylen = static_cast<long long>(xlen) + hlen - 1;
+  VS_REQUIRE(ylen < (1LL << 31), "vs_conv1d: output too long");
+  VS_REQUIRE(batch <= 1 || (xs >= xlen && ys >= ylen),
+             "vs_conv1d: row strides smaller than the rows");
+  VS_REQUIRE(hs == 0 || hs >= hlen, "vs_conv1d: filter stride < filter length");
+  VS_REQUIRE(batch <= 65535 || algo == VS_CONV_OVERLAP_SAVE,
+             "vs_conv1d: batch > 65535");
+  if (batch == 0) return VS_OK;
+  auto s = static_cast<hipStream_t>(stream);
+  if (algo == VS_CONV_AUTO) algo = conv::select(xlen, hlen, batch);
+  log(2, "vs_conv1d: x=%d h=%d batch=%d algo=%d", xlen, hlen, batch, algo);
+  switch (algo) {
+    case VS_CONV_DIRECT:
+      return conv::run_direct(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+    case VS_CONV_OVERLAP_SAVE:
+      if ((1 << conv::os_block_log(hlen)) > hlen - 1 + 16)
+        return conv::run_block(correlate, true, x, xlen, xs, h, hlen, hs, y, ys,
+                               batch, s);
+      log(1, "vs_conv1d: filter %d too long for an overlap-save block, using FFT",
+          hlen);
+      [[fallthrough]];
+    case VS_CONV_FFT: {
+      int lm = 1;
+      while ((1LL << lm) < ylen) lm++;
+      if (lm <= fft::kMaxLdsLog)
+        return conv::run_block(correlate, false, x, xlen, xs, h, hlen, hs, y, ys,
+                               batch, s);
+      return conv::run_fft_large(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+    }
+  }
+  set_error("vs_conv1d: unknown algorithm %d", algo);
+  return VS_ERR_INVALID;
+}
+
+}  // extern "C"

@@ -1,0 +1,350 @@
+// Decimated and stationary (a trous) wavelet transforms (SURVEY.md §2.3 K13,
+// K14) over the Daubechies / Symlet / Coiflet banks.
+//
+//   * single level (vs_dwt / vs_swt): a 256-thread block owns a tile of 1024
+//     outputs of one signal, stages the input window (tile + filter support,
+//     boundary extension applied on load) in LDS and every lane produces 4
+//     outputs.  The SWT touches only the `order` non-zero taps of the dilated
+//     filter (the reference expands it to order * 2^(level-1) taps,
+//     src/wavelet.c:211-246).  Taps live in the kernel-argument segment and
+//     are read with scalar loads.
+//   * multi-level (vs_swt_multilevel / vs_dwt_multilevel): one workgroup per
+//     signal keeps the running low-pass band in LDS across all levels and only
+//     writes each level's high band (and the final low band) to HBM: one HBM
+//     read of the input for L levels instead of L.
+//
+// Extension past the end of the signal follows the reference
+// (src/wavelet.c:248-269): periodic src[t % len], mirror
+// src[len - 1 - t % len], constant src[len - 1], zero.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "csrc/data/wavelet_tables.h"
+#include "csrc/kernels/device.h"
+#include "csrc/runtime/runtime.h"
+#include "simd/gpu.h"
+
+namespace vs {
+namespace wav {
+namespace {
+
+constexpr int kMaxOrder = wavelet_tables::kMaxOrder;
+
+struct Taps {
+  float lp[kMaxOrder];
+  float hp[kMaxOrder];
+  int order;
+};
+
+__device__ __forceinline__ int ext_index(int idx, int len, int ext) {
+  // Returns the source index for position idx (idx >= 0), or -1 for zero.
+  if (idx < len) return idx;
+  const int t = idx - len;
+  switch (ext) {
+    case EXTENSION_TYPE_PERIODIC: return t % len;
+    case EXTENSION_TYPE_MIRROR: return len - 1 - (t % len);
+    case EXTENSION_TYPE_CONSTANT: return len - 1;
+    default: return -1;
+  }
+}
+
+template <class P>
+__device__ __forceinline__ float ext_load(const P *src, int idx, int len, int ext) {
+  const int j = ext_index(idx, len, ext);
+  return j < 0 ? 0.f : static_cast<float>(src[j]);
+}
+
+constexpr int kThreads = 256;
+constexpr int kPer = 4;
+constexpr int kTile = kThreads * kPer;  // outputs per block
+
+// One decimated level: hi/lo[k] = sum_j hp/lp[j] * x~[2k + j], k < len/2.
+__global__ __launch_bounds__(kThreads) void dwt_kernel(
+    Taps taps, int ext, const float *__restrict__ src, int len, int64_t ss,
+    float *__restrict__ hi, float *__restrict__ lo, int64_t os) {
+  __shared__ float s[2 * kTile + kMaxOrder];
+  const float *x = src + blockIdx.y * ss;
+  const int half = len / 2;
+  const int k0 = blockIdx.x * kTile;
+  const int span = 2 * kTile + taps.order;
+  for (int i = threadIdx.x; i < span; i += kThreads) {
+    const int idx = 2 * k0 + i;
+    s[i] = idx < len + taps.order ? ext_load(x, idx, len, ext) : 0.f;
+  }
+  __syncthreads();
+  float* h = hi + blockIdx.y * os;
+  float* l = lo + blockIdx.y * os;
+#pragma unroll
+  for (int q = 0; q < kPer; q++) {
+    const int kk = threadIdx.x + q * kThreads;
+    float sh = 0.f, sl = 0.f;
+    for (int j = 0; j < taps.order; j++) {
+      const float v = s[2 * kk + j];
+      sh = fmaf(taps.hp[j], v, sh);
+      sl = fmaf(taps.lp[j], v, sl);
+    }
+    if (k0 + kk < half) {
+      h[k0 + kk] = sh;
+      l[k0 + kk] = sl;
+    }
+  }
+}
+
+// One stationary level with dilation `dil`: out[i] = sum_r c[r] x~[i + r dil].
+// The LDS window is kTile + (order-1)*dil samples; launched only when it fits.
+constexpr int kSwtLds = 12288;
+
+__global__ __launch_bounds__(kThreads) void swt_kernel(
+    Taps taps, int ext, int dil, const float *__restrict__ src, int len,
+    int64_t ss, float *__restrict__ hi, int64_t hs, float *__restrict__ lo,
+    int64_t ls) {
+  __shared__ float s[kSwtLds];
+  const float *x = src + blockIdx.y * ss;
+  const int i0 = blockIdx.x * kTile;
+  const int span = kTile + (taps.order - 1) * dil;
+  for (int i = threadIdx.x; i < span; i += kThreads)
+    s[i] = ext_load(x, i0 + i, len, ext);
+  __syncthreads();
+  float* h = hi + blockIdx.y * hs;
+  float* l = lo + blockIdx.y * ls;
+#pragma unroll
+  for (int q = 0; q < kPer; q++) {
+    const int ii = threadIdx.x + q * kThreads;
+    float sh = 0.f, sl = 0.f;
+    for (int r = 0; r < taps.order; r++) {
+      const float v = s[ii + r * dil];
+      sh = fmaf(taps.hp[r], v, sh);
+      sl = fmaf(taps.lp[r], v, sl);
+    }
+    if (i0 + ii < len) {
+      h[i0 + ii] = sh;
+      l[i0 + ii] = sl;
+    }
+  }
+}
+
+// Same without LDS staging, for dilations whose window does not fit.
+__global__ __launch_bounds__(kThreads) void swt_global_kernel(
+    Taps taps, int ext, int dil, const float *__restrict__ src, int len,
+    int64_t ss, float *__restrict__ hi, int64_t hs, float *__restrict__ lo,
+    int64_t ls) {
+  const float *x = src + blockIdx.y * ss;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= len) return;
+  float sh = 0.f, sl = 0.f;
+  for (int r = 0; r < taps.order; r++) {
+    const float v = ext_load(x, i + r * dil, len, ext);
+    sh = fmaf(taps.hp[r], v, sh);
+    sl = fmaf(taps.lp[r], v, sl);
+  }
+  hi[blockIdx.y * hs + i] = sh;
+  lo[blockIdx.y * ls + i] = sl;
+}
+
+// All `levels` stationary levels of one signal in LDS (two ping-pong bands).
+constexpr int kMultiMax = 8192;  // samples per signal held in LDS
+
+__global__ __launch_bounds__(1024) void swt_multi_kernel(
+    Taps taps, int ext, int levels, const float *__restrict__ src, int len,
+    float *__restrict__ hi, float *__restrict__ lo) {
+  __shared__ float band[2][kMultiMax];
+  const int64_t sig = blockIdx.x;
+  const float *x = src + sig * len;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) band[0][i] = x[i];
+  __syncthreads();
+  int cur = 0;
+  for (int l = 0; l < levels; l++) {
+    const int dil = 1 << l;
+    float *hrow = hi + (sig * levels + l) * len;
+    const float *in = band[cur];
+    float *out = band[cur ^ 1];
+    for (int i = threadIdx.x; i < len; i += blockDim.x) {
+      float sh = 0.f, sl = 0.f;
+      for (int r = 0; r < taps.order; r++) {
+        const float v = ext_load(in, i + r * dil, len, ext);
+        sh = fmaf(taps.hp[r], v, sh);
+        sl = fmaf(taps.lp[r], v, sl);
+      }
+      hrow[i] = sh;
+      out[i] = sl;
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  float *lrow = lo + sig * len;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) lrow[i] = band[cur][i];
+}
+
+// Mallat pyramid of one signal in LDS: out row = [hi_1 | hi_2 | ... | hi_L | lo_L].
+constexpr int kDwtMultiMax = 16384;
+
+__global__ __launch_bounds__(1024) void dwt_multi_kernel(
+    Taps taps, int ext, int levels, const float *__restrict__ src, int len,
+    float *__restrict__ out) {
+  __shared__ float band[kDwtMultiMax + kDwtMultiMax / 2];
+  const int64_t sig = blockIdx.x;
+  const float *x = src + sig * len;
+  float *orow = out + sig * len;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) band[i] = x[i];
+  __syncthreads();
+  int n = len, off = 0;
+  float *in = band, *nxt = band + kDwtMultiMax;
+  for (int l = 0; l < levels; l++) {
+    const int half = n / 2;
+    for (int k = threadIdx.x; k < half; k += blockDim.x) {
+      float sh = 0.f, sl = 0.f;
+      for (int j = 0; j < taps.order; j++) {
+        const float v = ext_load(in, 2 * k + j, n, ext);
+        sh = fmaf(taps.hp[j], v, sh);
+        sl = fmaf(taps.lp[j], v, sl);
+      }
+      orow[off + k] = sh;
+      nxt[k] = sl;
+    }
+    __syncthreads();
+    // the new low band becomes the input; copy it to the front half
+    for (int k = threadIdx.x; k < half; k += blockDim.x) in[k] = nxt[k];
+    __syncthreads();
+    off += half;
+    n = half;
+  }
+  for (int k = threadIdx.x; k < n; k += blockDim.x) orow[off + k] = in[k];
+}
+
+vs_status launch_swt(const Taps &t, int level, int ext, const float *src,
+                     int len, int64_t ss, float *hi, int64_t hs, float *lo,
+                     int64_t ls, int batch, hipStream_t s) {
+  const int dil = 1 << (level - 1);
+  const long long window = kTile + static_cast<long long>(t.order - 1) * dil;
+  if (window <= kSwtLds) {
+    const dim3 grid(static_cast<unsigned>((len + kTile - 1) / kTile),
+                    static_cast<unsigned>(batch));
+    hipLaunchKernelGGL(swt_kernel, grid, dim3(kThreads), 0, s, t, ext, dil, src, len,
+                       ss, hi, hs, lo, ls);
+  } else {
+    const dim3 grid(static_cast<unsigned>((len + kThreads - 1) / kThreads),
+                    static_cast<unsigned>(batch));
+    hipLaunchKernelGGL(swt_global_kernel, grid, dim3(kThreads), 0, s, t, ext, dil,
+                       src, len, ss, hi, hs, lo, ls);
+  }
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status make_taps(int type, int order, Taps *t) {
+  const auto wt = static_cast<WaveletType>(type);
+  const float *lp = wavelet_tables::lowpass_f(wt, order);
+  VS_REQUIRE(lp, "wavelet: unsupported (type %d, order %d)", type, order);
+  t->order = order;
+  wavelet_tables::make_filters(lp, order, t->hp, t->lp);
+  return VS_OK;
+}
+
+}  // namespace
+}  // namespace wav
+}  // namespace vs
+
+using namespace vs;
+using namespace vs::wav;
+
+extern "C" {
+
+vs_status vs_wavelet_filter(int type, int order, float *out) {
+  VS_REQUIRE(out, "vs_wavelet_filter: null pointer");
+  const float *lp = wavelet_tables::lowpass_f(static_cast<WaveletType>(type), order);
+  VS_REQUIRE(lp, "vs_wavelet_filter: unsupported (type %d, order %d)", type, order);
+  for (int i = 0; i < order; i++) out[i] = lp[i];
+  return VS_OK;
+}
+
+vs_status vs_dwt(int type, int order, int ext, const float *src, int len,
+                 int64_t ss, float *hi, float *lo, int64_t os, int batch,
+                 vs_stream_t stream) {
+  VS_REQUIRE(src && hi && lo, "vs_dwt: null pointer");
+  VS_REQUIRE(len > 0 && len % 2 == 0, "vs_dwt: length %d must be positive and even", len);
+  VS_REQUIRE(ext >= 0 && ext <= 3, "vs_dwt: bad extension %d", ext);
+  VS_REQUIRE(batch >= 0 && batch <= 65535, "vs_dwt: batch out of range");
+  if (batch == 0) return VS_OK;
+  Taps t;
+  VS_TRY(make_taps(type, order, &t));
+  const dim3 grid(static_cast<unsigned>((len / 2 + kTile - 1) / kTile),
+                  static_cast<unsigned>(batch));
+  hipLaunchKernelGGL(dwt_kernel, grid, dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), t, ext, src, len, ss, hi, lo, os);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+vs_status vs_swt(int type, int order, int level, int ext, const float *src,
+                 int len, int64_t ss, float *hi, float *lo, int64_t os, int batch,
+                 vs_stream_t stream) {
+  VS_REQUIRE(src && hi && lo, "vs_swt: null pointer");
+  VS_REQUIRE(len > 0, "vs_swt: empty input");
+  VS_REQUIRE(level >= 1 && level <= 24, "vs_swt: level %d out of range", level);
+  VS_REQUIRE(ext >= 0 && ext <= 3, "vs_swt: bad extension %d", ext);
+  VS_REQUIRE(batch >= 0 && batch <= 65535, "vs_swt: batch out of range");
+  if (batch == 0) return VS_OK;
+  Taps t;
+  VS_TRY(make_taps(type, order, &t));
+  return launch_swt(t, level, ext, src, len, ss, hi, os, lo, os, batch,
+                    static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
+                            const float *src, int len, float *hi, float *lo,
+                            int batch, vs_stream_t stream) {
+  VS_REQUIRE(src && hi && lo, "vs_swt_multilevel: null pointer");
+  VS_REQUIRE(levels >= 1 && levels <= 24, "vs_swt_multilevel: levels out of range");
+  VS_REQUIRE(len > 0, "vs_swt_multilevel: empty input");
+  VS_REQUIRE(batch >= 0, "vs_swt_multilevel: negative batch");
+  if (batch == 0) return VS_OK;
+  Taps t;
+  VS_TRY(make_taps(type, order, &t));
+  auto s = static_cast<hipStream_t>(stream);
+  if (len <= kMultiMax) {
+    const int threads = len >= 1024 ? 1024 : ((len + 63) / 64) * 64;
+    hipLaunchKernelGGL(swt_multi_kernel, dim3(static_cast<unsigned>(batch)),
+                       dim3(threads), 0, s, t, ext, levels, src, len, hi, lo);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+  }
+  // Long signals: level by level through HBM (lo of level l feeds level
+  // l+1, ping-ponging between two scratch bands; the last level writes lo).
+  VS_REQUIRE(batch <= 65535, "vs_swt_multilevel: batch out of range");
+  DeviceBuffer tmp;
+  const size_t band = static_cast<size_t>(len) * batch;
+  VS_TRY(tmp.alloc(2 * band * sizeof(float), s));
+  const float *in = src;
+  for (int l = 1; l <= levels; l++) {
+    float *dst = l == levels ? lo : tmp.as<float>() + (l % 2) * band;
+    VS_TRY(launch_swt(t, l, ext, in, len, len,
+                      hi + static_cast<int64_t>(l - 1) * len,
+                      static_cast<int64_t>(levels) * len, dst, len, batch, s));
+    in = dst;
+  }
+  return VS_OK;
+}
+
+vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,
+                            const float *src, int len, float *out, int batch,
+                            vs_stream_t stream) {
+  VS_REQUIRE(src && out, "vs_dwt_multilevel: null pointer");
+  VS_REQUIRE(levels >= 1 && len > 0 && len % (1 << levels) == 0,
+             "vs_dwt_multilevel: length %d not divisible by 2^%d", len, levels);
+  VS_REQUIRE(len <= kDwtMultiMax, "vs_dwt_multilevel: length %d > %d", len,
+             kDwtMultiMax);
+  VS_REQUIRE(batch >= 0, "vs_dwt_multilevel: negative batch");
+  if (batch == 0) return VS_OK;
+  Taps t;
+  VS_TRY(make_taps(type, order, &t));
+  const int threads = len / 2 >= 1024 ? 1024 : ((len / 2 + 63) / 64) * 64;
+  hipLaunchKernelGGL(dwt_multi_kernel, dim3(static_cast<unsigned>(batch)),
+                     dim3(threads), 0, static_cast<hipStream_t>(stream), t, ext,
+                     levels, src, len, out);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+"""Port of reference tests/wavelet.cc (goldens + parametrised sweeps) plus
+batched / multi-level device checks."""
+import numpy as np
+import pytest
+
+from veles.simd_amd import capi
+
+D, C, S = capi.WAVELET_TYPE_DAUBECHIES, capi.WAVELET_TYPE_COIFLET, capi.WAVELET_TYPE_SYMLET
+EXTS = [0, 1, 2, 3]
+
+VALID_LO = [1.42184071797210, 4.25026784271829, 7.07869496746448, 9.90712209221067,
+            12.7355492169569, 15.5639763417030, 18.3924034664492, 21.2208305911954,
+            24.0492577159416, 26.8776848406878, 29.7061119654340, 32.5345390901802,
+            35.3629662149264, 37.4782538234490, 45.3048707044478, 28.8405938767906]
+VALID_HI_TAIL = [-15.5030002317990, 5.58066496329142, -1.39137323046436]
+
+
+def _ulps(a, b):
+    a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b)
+
+
+def test_wavelet_apply_na_golden():
+    hi, lo = capi.wavelet_apply(D, 8, 0, np.arange(32, dtype=np.float32), na=True)
+    assert (_ulps(lo, np.float32(VALID_LO)) <= 4).all()
+    np.testing.assert_allclose(hi[:13], 0, atol=1e-5)
+    np.testing.assert_allclose(hi[13:], VALID_HI_TAIL, atol=1e-5)
+
+
+def test_stationary_wavelet_apply_na_golden():
+    x = np.arange(32, dtype=np.float32)
+    hi1, lo1 = capi.stationary_wavelet_apply(D, 8, 1, 0, x, na=True)
+    hi2, lo2 = capi.stationary_wavelet_apply(D, 8, 2, 0, lo1, na=True)
+    np.testing.assert_allclose(hi1[:25], 0, atol=1e-5)
+    np.testing.assert_allclose(hi1[25:], [7.37209002588238, -15.5030002317990,
+                                          4.68518434194794, 5.58066496329142,
+                                          -0.404449011712775, -1.39137323046436,
+                                          -0.339116857120903], atol=1e-5)
+    np.testing.assert_allclose(hi2[11:14], [-0.0781250000022623, 0.164291522328916,
+                                            0.634073488075181], atol=1e-5)
+    lo_valid = [6.03235928067132, 8.03235928067132, 10.0323592806713]
+    assert (_ulps(lo2[:3], np.float32(lo_valid)) <= 4).all()
+    np.testing.assert_allclose(lo2[-1], 5.73072526035035, rtol=1e-6)
+
+
+def test_validate_order():
+    v = capi.fn("wavelet_validate_order")
+    assert v(D, 8) and v(S, 76) and v(C, 30) and v(C, 6)
+    assert not v(D, 7) and not v(D, 78) and not v(C, 8) and not v(C, 36)
+
+
+def _params_dwt():
+    out = [(t, o, e) for t in (D, S) for o in (2, 4, 6, 8, 12, 16) for e in EXTS]
+    return out + [(C, o, e) for o in (6, 12) for e in EXTS]
+
+
+def _params_swt():
+    out = [(t, o, l, e) for t in (D, S) for o in (2, 4, 6, 8, 12, 16)
+           for l in (1, 2, 3, 4) for e in EXTS]
+    return out + [(C, o, l, e) for o in (6, 12) for l in (1, 2) for e in EXTS]
+
+
+@pytest.mark.parametrize("t,o,e", _params_dwt())
+def test_wavelet_apply_vs_na(t, o, e):
+    x = np.arange(512, dtype=np.float32)
+    hi, lo = capi.wavelet_apply(t, o, e, x)
+    vhi, vlo = capi.wavelet_apply(t, o, e, x, na=True)
+    np.testing.assert_allclose(hi, vhi, atol=5e-4)
+    np.testing.assert_allclose(lo, vlo, atol=5e-4)
+
+
+@pytest.mark.parametrize("t,o,l,e", _params_swt())
+def test_stationary_wavelet_apply_vs_na(t, o, l, e):
+    x = np.arange(512, dtype=np.float32)
+    hi, lo = capi.stationary_wavelet_apply(t, o, l, e, x)
+    vhi, vlo = capi.stationary_wavelet_apply(t, o, l, e, x, na=True)
+    np.testing.assert_allclose(hi, vhi, atol=5e-4)
+    np.testing.assert_allclose(lo, vlo, atol=5e-4)
+
+
+def test_filter_banks_orthonormal():
+    """Every generated bank is an orthonormal QMF with the reference scaling."""
+    import ctypes
+    lib = capi._lib.lib()
+    for t, orders, norm in ((D, range(2, 77, 2), np.sqrt(2)), (S, range(2, 77, 2), 1.0),
+                            (C, range(6, 31, 6), 1.0)):
+        for o in orders:
+            f = np.zeros(o, np.float32)
+            assert lib.vs_wavelet_filter(t, o, ctypes.c_void_p(f.ctypes.data)) == 0
+            h = f.astype(np.float64) * (np.sqrt(2) / norm)
+            assert abs(h.sum() - np.sqrt(2)) < 1e-5
+            for s in range(o // 2):
+                want = 1.0 if s == 0 else 0.0
+                assert abs(np.dot(h[:o - 2 * s], h[2 * s:]) - want) < 5e-5, (t, o, s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,o", [(D, 8), (S, 16), (C, 12), (D, 76)])
+@pytest.mark.parametrize("e", EXTS)
+def test_device_batched_and_multilevel(t, o, e):
+    import torch
+    from veles.simd_amd import ops
+    g = torch.Generator().manual_seed(o * 10 + e)
+    x = torch.randn(5, 2048, generator=g)
+    hi, lo = ops.dwt(x.cuda(), t, o, e)
+    for b in range(5):
+        vhi, vlo = capi.wavelet_apply(t, o, e, x[b].numpy(), na=True)
+        np.testing.assert_allclose(hi[b].cpu().numpy(), vhi, atol=1e-4)
+        np.testing.assert_allclose(lo[b].cpu().numpy(), vlo, atol=1e-4)
+    his, lof = ops.swt(x.cuda(), t, o, levels=4, ext=e)
+    cur = x.numpy()
+    for l in range(1, 5):
+        for b in range(5):
+            vhi, vlo = capi.stationary_wavelet_apply(t, o, l, e, cur[b], na=True)
+            np.testing.assert_allclose(his[b, l - 1].cpu().numpy(), vhi, atol=2e-4)
+            cur[b] = vlo
+    np.testing.assert_allclose(lof.cpu().numpy(), cur, atol=2e-4)
+    pyr = ops.wavedec(x.cuda(), t, o, levels=3, ext=e).cpu().numpy()
+    cur = x.numpy()
+    off = 0
+    for l in range(3):
+        n = cur.shape[1] // 2
+        nxt = np.zeros((5, n), np.float32)
+        for b in range(5):
+            vhi, vlo = capi.wavelet_apply(t, o, e, cur[b], na=True)
+            np.testing.assert_allclose(pyr[b, off:off + n], vhi, atol=2e-4)
+            nxt[b] = vlo
+        cur = nxt
+        off += n
+    np.testing.assert_allclose(pyr[:, off:], cur, atol=2e-4)

@@ -1,0 +1,324 @@
+"""Signal-processing ops: FFT, convolution / correlation, wavelets, peaks.
+
+References: src/convolve.c + src/correlate.c (conv1d), FFTF usage in
+src/convolve.c (fft / rfft / irfft), src/wavelet.c (dwt / swt / wavedec),
+src/detect_peaks.c (detect_peaks).  GPU tensors run the native HIP kernels;
+CPU tensors run an fp64-accumulated torch reference of the same math.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _lib
+from ._util import on_device, ptr, require_gpu_tensor, stream_of
+
+ALGORITHMS = {"auto": 0, "direct": 1, "fft": 2, "overlap_save": 3}
+
+
+def _algo(a) -> int:
+    return ALGORITHMS[a] if isinstance(a, str) else int(a)
+
+
+def _rows(t: torch.Tensor):
+    """(2-D contiguous view, original leading shape)."""
+    lead = t.shape[:-1]
+    return t.reshape(-1, t.shape[-1]).contiguous(), lead
+
+
+# ---------------------------------------------------------------- conv1d
+@torch.library.custom_op("veles::conv1d", mutates_args=())
+def _conv1d(x: torch.Tensor, h: torch.Tensor, algorithm: int,
+            correlate: bool) -> torch.Tensor:
+    if x.dtype != torch.float32 or h.dtype != torch.float32:
+        raise TypeError("veles::conv1d expects float32")
+    xr, lead = _rows(x)
+    batch, xlen = xr.shape
+    hr = h.reshape(-1, h.shape[-1]).contiguous()
+    hlen = hr.shape[1]
+    if hr.shape[0] not in (1, batch):
+        raise ValueError("veles::conv1d: filters must be 1 or one per signal")
+    ylen = xlen + hlen - 1
+    if not x.is_cuda:
+        # torch conv1d is a correlation: weight = h for correlation,
+        # flip(h) for convolution (reference definitions, see module doc).
+        w = hr.double() if correlate else hr.double().flip(-1)
+        if hr.shape[0] == 1:
+            out = torch.nn.functional.conv1d(xr.double()[:, None], w[None],
+                                             padding=hlen - 1)[:, 0]
+        else:
+            out = torch.nn.functional.conv1d(xr.double()[None], w[:, None],
+                                             padding=hlen - 1, groups=batch)[0]
+        return out.float().reshape(*lead, ylen)
+    require_gpu_tensor(x, "veles::conv1d")
+    y = torch.empty((batch, ylen), dtype=torch.float32, device=x.device)
+    with on_device(x):
+        _lib.call("vs_conv1d", algorithm, int(correlate), ptr(xr), xlen, xlen,
+                  ptr(hr), hlen, hlen if hr.shape[0] > 1 else 0, ptr(y), ylen,
+                  batch, stream_of(x))
+    return y.reshape(*lead, ylen)
+
+
+@_conv1d.register_fake
+def _(x, h, algorithm, correlate):
+    return x.new_empty((*x.shape[:-1], x.shape[-1] + h.shape[-1] - 1))
+
+
+def conv1d(x: torch.Tensor, h: torch.Tensor, algorithm="auto",
+           correlate: bool = False) -> torch.Tensor:
+    """Full linear convolution (or cross-correlation) of every row of x with
+    h (one shared filter, or one per row).  Output length x + h - 1."""
+    return _conv1d(x, h, _algo(algorithm), bool(correlate))
+
+
+def correlate(x, h, algorithm="auto"):
+    return _conv1d(x, h, _algo(algorithm), True)
+
+
+def conv1d_algorithm(xlen: int, hlen: int, batch: int = 1) -> str:
+    """The algorithm "auto" resolves to on the GPU for this shape."""
+    a = _lib.lib().vs_conv1d_select(xlen, hlen, batch)
+    return {1: "direct", 2: "fft", 3: "overlap_save"}[a]
+
+
+# ------------------------------------------------------------------- FFT
+@torch.library.custom_op("veles::fft", mutates_args=())
+def fft(z: torch.Tensor, inverse: bool = False) -> torch.Tensor:
+    """Unnormalised complex FFT over the second-to-last dim of a float32
+    tensor [..., n, 2] (interleaved re/im); n a power of two <= 2^24."""
+    if z.shape[-1] != 2:
+        raise ValueError("veles::fft expects [..., n, 2] interleaved complex")
+    n = z.shape[-2]
+    if not z.is_cuda:
+        c = torch.view_as_complex(z.contiguous().double())
+        r = torch.fft.ifft(c, dim=-1) * n if inverse else torch.fft.fft(c, dim=-1)
+        return torch.view_as_real(r).float()
+    require_gpu_tensor(z, "veles::fft")
+    zc = z.contiguous()
+    out = torch.empty_like(zc)
+    batch = zc.numel() // (2 * n)
+    with on_device(z):
+        _lib.call("vs_fft_c2c", ptr(zc), ptr(out), n, batch, int(inverse),
+                  stream_of(z))
+    return out
+
+
+@fft.register_fake
+def _(z, inverse=False):
+    return torch.empty_like(z)
+
+
+@torch.library.custom_op("veles::rfft", mutates_args=())
+def rfft(x: torch.Tensor) -> torch.Tensor:
+    """Real FFT of the last dim (n a power of two): [..., n/2+1, 2]."""
+    n = x.shape[-1]
+    if not x.is_cuda:
+        return torch.view_as_real(torch.fft.rfft(x.double(), dim=-1)).float()
+    require_gpu_tensor(x, "veles::rfft")
+    xc = x.contiguous()
+    out = torch.empty((*x.shape[:-1], n // 2 + 1, 2), dtype=torch.float32,
+                      device=x.device)
+    with on_device(x):
+        _lib.call("vs_fft_r2c", ptr(xc), ptr(out), n, xc.numel() // n, stream_of(x))
+    return out
+
+
+@rfft.register_fake
+def _(x):
+    return x.new_empty((*x.shape[:-1], x.shape[-1] // 2 + 1, 2))
+
+
+@torch.library.custom_op("veles::irfft", mutates_args=())
+def irfft(X: torch.Tensor, n: int) -> torch.Tensor:
+    """Unnormalised inverse of rfft (returns n * x, the FFTF convention)."""
+    if not X.is_cuda:
+        c = torch.view_as_complex(X.contiguous().double())
+        return (torch.fft.irfft(c, n=n, dim=-1) * n).float()
+    require_gpu_tensor(X, "veles::irfft")
+    Xc = X.contiguous()
+    out = torch.empty((*X.shape[:-2], n), dtype=torch.float32, device=X.device)
+    with on_device(X):
+        _lib.call("vs_fft_c2r", ptr(Xc), ptr(out), n, out.numel() // n, stream_of(X))
+    return out
+
+
+@irfft.register_fake
+def _(X, n):
+    return X.new_empty((*X.shape[:-2], n))
+
+
+# -------------------------------------------------------------- wavelets
+DAUBECHIES, COIFLET, SYMLET = 0, 1, 2
+PERIODIC, MIRROR, CONSTANT, ZERO = 0, 1, 2, 3
+_FAMILY = {"daubechies": 0, "db": 0, "coiflet": 1, "coif": 1, "symlet": 2, "sym": 2}
+_EXT = {"periodic": 0, "mirror": 1, "constant": 2, "zero": 3}
+
+
+def _fam(t):
+    return _FAMILY[t] if isinstance(t, str) else int(t)
+
+
+def _ext(e):
+    return _EXT[e] if isinstance(e, str) else int(e)
+
+
+def wavelet_filter(family, order: int) -> torch.Tensor:
+    """The library's float32 low-pass taps (reference normalisation)."""
+    import ctypes
+    out = torch.empty(order, dtype=torch.float32)
+    _lib.check(_lib.lib().vs_wavelet_filter(_fam(family), order,
+                                            ctypes.c_void_p(out.data_ptr())),
+               "vs_wavelet_filter")
+    return out
+
+
+def _extend_host(x: torch.Tensor, size: int, ext: int) -> torch.Tensor:
+    n = x.shape[-1]
+    t = torch.arange(size)
+    if ext == PERIODIC:
+        e = x[..., t % n]
+    elif ext == MIRROR:
+        e = x[..., n - 1 - (t % n)]
+    elif ext == CONSTANT:
+        e = x[..., -1:].expand(*x.shape[:-1], size)
+    else:
+        e = torch.zeros(*x.shape[:-1], size, dtype=x.dtype)
+    return torch.cat([x, e], dim=-1)
+
+
+def _qmf(lp: torch.Tensor) -> torch.Tensor:
+    o = lp.shape[0]
+    sign = torch.tensor([1.0 if (i & 1) else -1.0 for i in range(o)], dtype=lp.dtype)
+    return (lp * sign).flip(0)
+
+
+@torch.library.custom_op("veles::dwt", mutates_args=())
+def _dwt(x: torch.Tensor, family: int, order: int, ext: int) -> torch.Tensor:
+    xr, lead = _rows(x)
+    batch, n = xr.shape
+    if not x.is_cuda:
+        lp = wavelet_filter(family, order).double()
+        hp = _qmf(lp)
+        xe = _extend_host(xr.double(), order, ext)
+        win = xe.unfold(-1, order, 2)[:, : n // 2]
+        return torch.stack([win @ hp, win @ lp]).float().reshape(2, *lead, n // 2)
+    require_gpu_tensor(x, "veles::dwt")
+    out = torch.empty((2, batch, n // 2), dtype=torch.float32, device=x.device)
+    with on_device(x):
+        _lib.call("vs_dwt", family, order, ext, ptr(xr), n, n, ptr(out[0]),
+                  ptr(out[1]), n // 2, batch, stream_of(x))
+    return out.reshape(2, *lead, n // 2)
+
+
+@_dwt.register_fake
+def _(x, family, order, ext):
+    return x.new_empty((2, *x.shape[:-1], x.shape[-1] // 2))
+
+
+def dwt(x, family="daubechies", order=8, ext="periodic"):
+    """One decimated level over the last dim: (hi, lo), each length n/2."""
+    r = _dwt(x, _fam(family), order, _ext(ext))
+    return r[0], r[1]
+
+
+@torch.library.custom_op("veles::swt", mutates_args=())
+def _swt(x: torch.Tensor, family: int, order: int, levels: int,
+         ext: int) -> torch.Tensor:
+    xr, lead = _rows(x)
+    batch, n = xr.shape
+    if not x.is_cuda:
+        lp = wavelet_filter(family, order).double()
+        hp = _qmf(lp)
+        cur = xr.double()
+        his = []
+        for lvl in range(levels):
+            dil = 1 << lvl
+            xe = _extend_host(cur, order * dil, ext)
+            idx = torch.arange(n)[:, None] + dil * torch.arange(order)[None, :]
+            win = xe[:, idx]
+            his.append(win @ hp)
+            cur = win @ lp
+        out = torch.cat([torch.stack(his, 1), cur[:, None]], 1).float()
+        return out.reshape(*lead, levels + 1, n)
+    require_gpu_tensor(x, "veles::swt")
+    out = torch.empty((batch, levels + 1, n), dtype=torch.float32, device=x.device)
+    hi = torch.empty((batch, levels, n), dtype=torch.float32, device=x.device)
+    lo = torch.empty((batch, n), dtype=torch.float32, device=x.device)
+    with on_device(x):
+        _lib.call("vs_swt_multilevel", family, order, levels, ext, ptr(xr), n,
+                  ptr(hi), ptr(lo), batch, stream_of(x))
+    out[:, :levels] = hi
+    out[:, levels] = lo
+    return out.reshape(*lead, levels + 1, n)
+
+
+@_swt.register_fake
+def _(x, family, order, levels, ext):
+    return x.new_empty((*x.shape[:-1], levels + 1, x.shape[-1]))
+
+
+def swt(x, family="daubechies", order=8, levels=1, ext="periodic"):
+    """Fused multi-level stationary DWT over the last dim.  Returns
+    (hi [..., levels, n], lo [..., n])."""
+    r = _swt(x, _fam(family), order, levels, _ext(ext))
+    return r[..., :levels, :], r[..., levels, :]
+
+
+@torch.library.custom_op("veles::wavedec", mutates_args=())
+def _wavedec(x: torch.Tensor, family: int, order: int, levels: int,
+             ext: int) -> torch.Tensor:
+    xr, lead = _rows(x)
+    batch, n = xr.shape
+    if not x.is_cuda:
+        parts, cur = [], xr
+        for _ in range(levels):
+            r = _dwt(cur, family, order, ext)
+            parts.append(r[0])
+            cur = r[1]
+        return torch.cat(parts + [cur], -1).reshape(*lead, n)
+    require_gpu_tensor(x, "veles::wavedec")
+    out = torch.empty((batch, n), dtype=torch.float32, device=x.device)
+    with on_device(x):
+        _lib.call("vs_dwt_multilevel", family, order, levels, ext, ptr(xr), n,
+                  ptr(out), batch, stream_of(x))
+    return out.reshape(*lead, n)
+
+
+@_wavedec.register_fake
+def _(x, family, order, levels, ext):
+    return torch.empty_like(x)
+
+
+def wavedec(x, family="daubechies", order=8, levels=1, ext="periodic"):
+    """Fused Mallat pyramid: rows [hi_1 | hi_2 | ... | hi_L | lo_L]."""
+    return _wavedec(x, _fam(family), order, levels, _ext(ext))
+
+
+# ----------------------------------------------------------------- peaks
+MAXIMUM, MINIMUM, BOTH = 1, 2, 3
+
+
+def detect_peaks(x: torch.Tensor, kind=BOTH):
+    """Strict extrema of a 1-D float32 tensor: (positions int32, values)."""
+    kind = {"max": 1, "min": 2, "both": 3}.get(kind, kind)
+    if not x.is_cuda:
+        xd = x.float()
+        d1 = xd[1:-1] - xd[:-2]
+        d2 = xd[1:-1] - xd[2:]
+        m = (d1 * d2) > 0
+        m &= ((d1 > 0) & bool(kind & 1)) | ((d1 < 0) & bool(kind & 2))
+        pos = torch.nonzero(m).flatten().int() + 1
+        return pos, xd[pos.long()]
+    require_gpu_tensor(x, "veles::detect_peaks")
+    xc = x.contiguous()
+    n = xc.numel()
+    cnt = torch.zeros(1, dtype=torch.int64, device=x.device)
+    with on_device(x):
+        s = stream_of(x)
+        _lib.call("vs_detect_peaks", ptr(xc), n, kind, None, None, 0, ptr(cnt), s)
+        total = int(cnt.item())
+        pos = torch.empty(total, dtype=torch.int32, device=x.device)
+        val = torch.empty(total, dtype=torch.float32, device=x.device)
+        if total:
+            _lib.call("vs_detect_peaks", ptr(xc), n, kind, ptr(pos), ptr(val), total,
+                      ptr(cnt), s)
+    return pos, val
