@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 
 #include "csrc/kernels/device.h"
 #include "csrc/kernels/fft_core.h"
@@ -83,7 +84,8 @@ __global__ __launch_bounds__(kDirThreads) void direct_kernel(
     const int top = q0 + kDirTaps;
 #pragma unroll
     for (int r = 0; r < kDirPerThread; r++) w[kDirPerThread + r] = sx[xpad(top + r)];
-    for (int mm = 0; mm < kDirTaps; mm += kDirPerThread) {
+    const int tap_end = (taps + kDirPerThread - 1) & ~(kDirPerThread - 1);
+    for (int mm = 0; mm < tap_end; mm += kDirPerThread) {
 #pragma unroll
       for (int r = 0; r < kDirPerThread; r++)
         w[r] = sx[xpad(top - mm - kDirPerThread + r)];
@@ -253,6 +255,10 @@ __global__ __launch_bounds__(256) void spectrum_mul_kernel(
 
 }  // namespace
 
+// Tuning knob (vs_tune_set("os_block_log_max", n)): cap of the overlap-save
+// block size, for A/B measurements.
+int g_os_log_max = fft::kMaxLdsLog;
+
 int os_block_log(int hlen) {
   // Reference block size 2^(floor(log2 M) + 2) (src/convolve.c:116-121),
   // raised to >= 2048 so every block amortises its transform over >= ~75%
@@ -261,7 +267,8 @@ int os_block_log(int hlen) {
   int m = hlen;
   while (m >>= 1) lg++;
   if (lg < 11) lg = 11;
-  if (lg > fft::kMaxLdsLog) lg = fft::kMaxLdsLog;
+  if (lg > g_os_log_max) lg = g_os_log_max;
+  while ((1 << lg) <= hlen && lg < fft::kMaxLdsLog) lg++;  // must exceed h - 1
   return lg;
 }
 
@@ -410,6 +417,17 @@ int vs_conv1d_select(int xlen, int hlen, int batch) {
 }
 
 int vs_conv1d_os_block(int hlen) { return 1 << conv::os_block_log(hlen); }
+
+vs_status vs_tune_set(const char *key, int value) {
+  VS_REQUIRE(key, "vs_tune_set: null key");
+  if (std::strcmp(key, "os_block_log_max") == 0) {
+    VS_REQUIRE(value >= 4 && value <= fft::kMaxLdsLog, "os_block_log_max out of range");
+    conv::g_os_log_max = value;
+    return VS_OK;
+  }
+  set_error("vs_tune_set: unknown key '%s'", key);
+  return VS_ERR_INVALID;
+}
 
 vs_status vs_conv1d(int algo, int correlate, const float *x, int xlen,
                     int64_t xs, const float *h, int hlen, int64_t hs, float *y,

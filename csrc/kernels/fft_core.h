@@ -2,8 +2,8 @@
 //
 // One signal of N = 2^LOGN complex points (N <= 16384) lives in LDS
 // (float2, one pad slot per 16 elements to break the power-of-two strides
-// of the early passes) while TPS = N/16 threads each own 16 points in
-// registers.  Each pass is a radix-R Stockham step (R in {2,4,8,16}):
+// of the early passes) while TPS = N/E threads each own E = 16 (32 at
+// N = 16384) points in registers.  Each pass is a radix-R Stockham step (R in {2,4,8,16}):
 //   butterfly i in [0, N/R), k = i mod P (P = product of earlier radices):
 //     u_j = x[i + j N/R] * w^(j k),  w = exp(-+2 pi i / (P R))
 //     v   = DFT_R(u)
@@ -145,7 +145,10 @@ template <int LOGN_>
 struct Plan {
   static constexpr int LOGN = LOGN_;
   static constexpr int N = 1 << LOGN;
-  static constexpr int E = LOGN >= 4 ? 16 : N;     // points per thread
+  // Points per thread: 16, or 32 at N = 16384 so the 512-thread workgroup
+  // keeps its working set in registers (at 1024 threads the 128-VGPR budget
+  // of 4 waves/SIMD spilled).
+  static constexpr int E = LOGN >= 14 ? 32 : (LOGN >= 4 ? 16 : N);
   static constexpr int TPS = N / E;                // threads per signal
   static constexpr int SMALL = LOGN >= 4 ? LOGN % 4 : 0;
   static constexpr int NPASS = LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1;
@@ -181,11 +184,24 @@ struct Pass {
     for (int b = 0; b < NB; b++) {
       const int i = t + b * PL::TPS;
       if constexpr (P > 1) {
+        // w^j (j < R) as the product of the table entries w, w^2, w^4, w^8
+        // selected by the bits of j: 4 gathers instead of R - 1 and only 4
+        // live twiddles (at most 3 products, <= ~3 ulp).
         const int k = i & (P - 1);
         constexpr int S = PL::N / (P * R);
+        float2 wb[4];
+#pragma unroll
+        for (int q = 0; (1 << q) < R; q++) wb[q] = tw[(1 << q) * k * S];
 #pragma unroll
         for (int j = 1; j < R; j++) {
-          const float2 w = tw[j * k * S];
+          float2 w = make_float2(1.f, 0.f);
+          bool first = true;
+#pragma unroll
+          for (int q = 0; (1 << q) < R; q++)
+            if (j & (1 << q)) {
+              w = first ? wb[q] : cmul(w, wb[q]);
+              first = false;
+            }
           v[b * R + j] = INV ? cmulc(v[b * R + j], w) : cmul(v[b * R + j], w);
         }
       }

@@ -162,6 +162,9 @@ vs_status vs_conv1d(int algo, int correlate, const float *x, int x_len,
 int vs_conv1d_select(int x_len, int h_len, int batch);
 /// Overlap-save block length the library uses for filter length h_len.
 int vs_conv1d_os_block(int h_len);
+/// Tuning knobs for measurements ("os_block_log_max": cap of the
+/// overlap-save block, log2).
+vs_status vs_tune_set(const char *key, int value);
 
 /* -------------------------------------------------------------- wavelets */
 /// Batched single-level decimated DWT: hi/lo rows of len/2 (stride

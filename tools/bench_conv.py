@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Conv1d throughput sweep (Msamples/s of input) over algorithms, filter
+lengths and overlap-save block caps, interleaved in one process."""
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from veles.simd_amd import _lib  # noqa: E402
+
+lib = _lib.lib()
+lib.vs_tune_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
+
+
+def main():
+    xlen = int(os.environ.get("XLEN", 1 << 20))
+    batch = int(os.environ.get("BATCH", 64))
+    rounds = int(os.environ.get("ROUNDS", 5))
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    x = torch.randn(batch, xlen, device="cuda")
+    res = {}
+    for hlen in [16, 64, 512, 4096]:
+        h = torch.randn(hlen, device="cuda")
+        ylen = xlen + hlen - 1
+        y = torch.empty(batch, ylen, device="cuda")
+        variants = [("auto", 0, 14), ("direct", 1, 14), ("fft", 2, 14)]
+        variants += [(f"os{lg}", 3, lg) for lg in (11, 12, 13, 14) if (1 << lg) > hlen + 64]
+        times = {v[0]: [] for v in variants}
+        ev0, ev1 = torch.cuda.Event(True), torch.cuda.Event(True)
+        for r in range(rounds):
+            for name, algo, lg in variants:
+                lib.vs_tune_set(b"os_block_log_max", lg)
+                run = lambda: lib.vs_conv1d(algo, 0, x.data_ptr(), xlen, xlen, h.data_ptr(),
+                                            hlen, 0, y.data_ptr(), ylen, batch, s)
+                assert run() == 0, lib.vs_last_error()
+                reps = 3
+                ev0.record()
+                for _ in range(reps):
+                    run()
+                ev1.record()
+                torch.cuda.synchronize()
+                times[name].append(ev0.elapsed_time(ev1) / reps)
+        lib.vs_tune_set(b"os_block_log_max", 14)
+        out = {k: round(xlen * batch / statistics.median(v) / 1e3, 1) for k, v in times.items()}
+        res[hlen] = out
+        print(f"h={hlen}: Msamples/s", out, flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
