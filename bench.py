@@ -76,7 +76,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist_on = world > 1
+    # Under torchrun (RANK set) always bring up the RCCL group, even at N=1,
+    # so the timed region's barrier / max-reduction is the same code at every N.
+    dist_on = "RANK" in os.environ
     torch.cuda.set_device(local)
     if dist_on:
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -11,12 +11,13 @@ from .elementwise import (add, affine, binary, complex_conjugate,  # noqa: F401
                           complex_multiply, convert, cos, exp, log, math,
                           minmax, mul, normalize2d, saxpy, sin, sub, sum_all)
 from .signal import (conv1d, conv1d_algorithm, correlate, detect_peaks,  # noqa: F401
-                     dwt, fft, irfft, rfft, swt, wavedec, wavelet_filter)
+                     dwt, fft, irfft, rfft, swt, swt_level, wavedec,
+                     wavelet_filter)
 
 __all__ = [
     "sgemm", "matmul", "matmul_transposed", "convert", "binary", "add", "sub",
     "mul", "complex_multiply", "complex_conjugate", "affine", "saxpy", "math",
     "sin", "cos", "log", "exp", "sum_all", "minmax", "normalize2d", "conv1d",
     "correlate", "conv1d_algorithm", "fft", "rfft", "irfft", "dwt", "swt",
-    "wavedec", "wavelet_filter", "detect_peaks",
+    "wavedec", "wavelet_filter", "detect_peaks", "swt_level",
 ]

@@ -263,6 +263,38 @@ def swt(x, family="daubechies", order=8, levels=1, ext="periodic"):
     return r[..., :levels, :], r[..., levels, :]
 
 
+@torch.library.custom_op("veles::swt_level", mutates_args=())
+def _swt_level(x: torch.Tensor, family: int, order: int, level: int,
+               ext: int) -> torch.Tensor:
+    xr, lead = _rows(x)
+    batch, n = xr.shape
+    if not x.is_cuda:
+        lp = wavelet_filter(family, order).double()
+        hp = _qmf(lp)
+        dil = 1 << (level - 1)
+        xe = _extend_host(xr.double(), order * dil, ext)
+        idx = torch.arange(n)[:, None] + dil * torch.arange(order)[None, :]
+        win = xe[:, idx]
+        return torch.stack([win @ hp, win @ lp]).float().reshape(2, *lead, n)
+    require_gpu_tensor(x, "veles::swt_level")
+    out = torch.empty((2, batch, n), dtype=torch.float32, device=x.device)
+    with on_device(x):
+        _lib.call("vs_swt", family, order, level, ext, ptr(xr), n, n, ptr(out[0]),
+                  ptr(out[1]), n, batch, stream_of(x))
+    return out.reshape(2, *lead, n)
+
+
+@_swt_level.register_fake
+def _(x, family, order, level, ext):
+    return x.new_empty((2, *x.shape))
+
+
+def swt_level(x, family="daubechies", order=8, level=1, ext="periodic"):
+    """One stationary level (filters dilated by 2^(level-1)): (hi, lo)."""
+    r = _swt_level(x, _fam(family), order, level, _ext(ext))
+    return r[0], r[1]
+
+
 @torch.library.custom_op("veles::wavedec", mutates_args=())
 def _wavedec(x: torch.Tensor, family: int, order: int, levels: int,
              ext: int) -> torch.Tensor:

@@ -1,0 +1,70 @@
+"""1-D row-split batched SGEMM over ranks (BASELINE
+config 5: batched SGEMM 8192^2 x 64 row-split across 8 GPUs with an RCCL
+all-gather over xGMI).
+
+C_i = A_i @ B_i for a batch of matrices.  Every rank owns a contiguous block
+of rows of every A_i and the whole B_i (replicated, or streamed from `src` by
+per-matrix broadcasts); it computes its rows of C_i with the MFMA SGEMM and
+the full C_i is assembled by one all-gather per matrix.  Collectives are
+issued asynchronously (RCCL runs them on its own stream, ordered after the
+producing kernel), so the all-gather of C_i overlaps the SGEMM of C_{i+1} and
+the broadcast of B_{i+1} is in flight while C_i is computed.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from . import comm
+
+
+def rowsplit_bmm(a_local: torch.Tensor, b: torch.Tensor | None, *,
+                 n: int | None = None, gather: bool = True,
+                 broadcast_src: int | None = None,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Row-split batched matmul.
+
+    a_local: [batch, m_local, k] -- this rank's rows (equal on every rank).
+    b:       [batch, k, n] replicated on every rank, or (broadcast_src set)
+             only meaningful on rank broadcast_src; other ranks may pass None
+             together with `n`.
+    gather:  return the full C [batch, m_local * world, n] on every rank
+             (else this rank's rows [batch, m_local, n]).
+    """
+    world = comm.world_size()
+    batch, m_loc, k = a_local.shape
+    if b is not None:
+        n = b.shape[-1]
+    if n is None:
+        raise ValueError("rowsplit_bmm: pass b or n")
+    if broadcast_src is not None and world > 1 and comm.rank() != broadcast_src:
+        b = torch.empty((batch, k, n), dtype=a_local.dtype, device=a_local.device)
+    if not gather or world == 1:
+        if broadcast_src is not None and world > 1:
+            dist.broadcast(b, broadcast_src)
+        return torch.stack([ops.sgemm(a_local[i], b[i]) for i in range(batch)]) \
+            if batch else a_local.new_empty((0, m_loc, n))
+    if out is None:
+        out = torch.empty((batch, m_loc * world, n), dtype=a_local.dtype,
+                          device=a_local.device)
+    pending = []
+    bcast = {}
+
+    def issue_bcast(i):
+        if broadcast_src is not None and i < batch:
+            bcast[i] = dist.broadcast(b[i], broadcast_src, async_op=True)
+
+    issue_bcast(0)
+    for i in range(batch):
+        issue_bcast(i + 1)  # prefetch the next B while computing this one
+        if i in bcast:
+            bcast.pop(i).wait()
+        c_loc = ops.sgemm(a_local[i], b[i])
+        pending.append((dist.all_gather_into_tensor(out[i], c_loc, async_op=True), c_loc))
+        if len(pending) > 2:  # bound the number of in-flight result shards
+            w, _ = pending.pop(0)
+            w.wait()
+    for w, _ in pending:
+        w.wait()
+    return out
