@@ -148,8 +148,15 @@ def main():
     base = _baseline()
     vs_base = None
     if base.get("sgemm_4096_gflops"):
-        vs_base = round(gflops / base["sgemm_4096_gflops"], 2)
+        # The reference publishes no numbers; this is its own
+        # AVX code measured on one host core (tools/measure_reference_cpu.py).
+        vs_base = round(gflops / base["sgemm_4096_gflops"], 1)
         secondary["baseline_source"] = base.get("source")
+        secondary["baseline_sgemm_gflops"] = base["sgemm_4096_gflops"]
+        ref_conv = base.get("conv_direct_2^20x4096_msamples_per_s")
+        if ref_conv and "conv1d_msamples_per_s" in secondary:
+            secondary["conv1d_vs_baseline"] = round(
+                secondary["conv1d_msamples_per_s"] / ref_conv, 1)
 
     if rank == 0:
         print(json.dumps({

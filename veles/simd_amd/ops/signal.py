@@ -63,6 +63,35 @@ def _(x, h, algorithm, correlate):
     return x.new_empty((*x.shape[:-1], x.shape[-1] + h.shape[-1] - 1))
 
 
+def _conv_setup(ctx, inputs, output):
+    x, h, algorithm, corr = inputs
+    ctx.save_for_backward(x, h)
+    ctx.algorithm = algorithm
+    ctx.corr = corr
+
+
+def _conv_backward(ctx, g):
+    """y = x (*) k with k = h (convolution) or flip(h) (correlation).
+    dx = valid correlation of g with k; dk = valid correlation of g with x."""
+    x, h = ctx.saved_tensors
+    k = h.flip(-1) if ctx.corr else h
+    X, H = x.shape[-1], k.shape[-1]
+    gx = gh = None
+    if ctx.needs_input_grad[0]:
+        r = _conv1d(g.contiguous(), k.contiguous(), ctx.algorithm, True)
+        gx = r[..., H - 1: H - 1 + X]
+    if ctx.needs_input_grad[1]:
+        gr = g.reshape(-1, g.shape[-1]).contiguous()
+        xr = x.reshape(-1, X).contiguous()
+        r = _conv1d(gr, xr, 0, True)[..., X - 1: X - 1 + H]
+        dk = r.sum(0) if h.dim() == 1 else r.reshape(h.shape)
+        gh = dk.flip(-1) if ctx.corr else dk
+    return gx, gh, None, None
+
+
+_conv1d.register_autograd(_conv_backward, setup_context=_conv_setup)
+
+
 def conv1d(x: torch.Tensor, h: torch.Tensor, algorithm="auto",
            correlate: bool = False) -> torch.Tensor:
     """Full linear convolution (or cross-correlation) of every row of x with

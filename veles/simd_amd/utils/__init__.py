@@ -1,0 +1,4 @@
+"""Utilities: GPU timing, profiler ranges, runtime configuration."""
+from .config import Config, config  # noqa: F401
+from .profiling import range_pop, range_push, trace_range  # noqa: F401
+from .timing import GpuTimer, benchmark  # noqa: F401
