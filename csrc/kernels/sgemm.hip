@@ -218,6 +218,233 @@ __global__ __launch_bounds__(C::kThreads) void sgemm_kernel(GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------
+// Generation 2: K-contiguous LDS images + 16-byte fragment reads.
+//
+// Both operand tiles are stored k-contiguous in LDS ([m][k] and [n][k],
+// pitch BK + 4 floats: conflict-free ds_read_b128 for 16 consecutive rows).
+// The 32x32x2 MFMA consumes two k per instruction (lane half h gets one);
+// since the order of the K sum is free, MFMA s (s = 0..3) of an 8-k group
+// takes k = 4h + s, so every lane fetches its 4 k values for 4 MFMAs with
+// ONE ds_read_b128 per operand tile (4x fewer LDS instructions than gen 1).
+// Fragments of group g+1 are read while the MFMAs of group g run, interior
+// tiles use unguarded 16-byte global loads, edge tiles a guarded copy of the
+// same loop (uniform branch per workgroup).
+template <int BM_, int BN_, int BK_, int WM_, int WN_>
+struct Cfg2 {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int TM = BM / WM / 32;
+  static constexpr int TN = BN / WN / 32;
+  static constexpr int P = BK + 4;  // LDS pitch (floats) of both images
+  static constexpr int kBuf = (BM + BN) * P;
+  static constexpr int kLdsFloats = 2 * kBuf;
+  static_assert(BK % 8 == 0, "BK must be a multiple of 8");
+};
+
+// Stage one operand tile (BMN rows of the op, BK deep) into registers.
+//   KC: stored [mn][k] (k contiguous)  -> float4 along k, no transpose.
+//   else: stored [k][mn]               -> float4 along mn, transposed on store.
+template <int BMN, int BK, int THREADS, bool KC>
+struct TileIO2 {
+  static constexpr int kLoads = BMN * BK / 4 / THREADS;
+  static_assert(kLoads * 4 * THREADS == BMN * BK, "tile not divisible");
+
+  template <bool GUARD>
+  __device__ static void load(const float *__restrict__ p, int64_t ld, int mn0,
+                             int mn_lim, int k0, int k_lim, bool vec,
+                             float4 (&r)[kLoads]) {
+#pragma unroll
+    for (int l = 0; l < kLoads; l++) {
+      const int idx = threadIdx.x + l * THREADS;
+      int mn, kk;
+      if (KC) {
+        mn = mn0 + idx / (BK / 4);
+        kk = k0 + (idx % (BK / 4)) * 4;
+      } else {
+        kk = k0 + idx / (BMN / 4);
+        mn = mn0 + (idx % (BMN / 4)) * 4;
+      }
+      const float *base = KC ? p + mn * ld + kk : p + kk * ld + mn;
+      if (!GUARD) {
+        r[l] = *reinterpret_cast<const float4 *>(base);
+      } else {
+        const bool full = KC ? (mn < mn_lim && kk + 3 < k_lim)
+                             : (kk < k_lim && mn + 3 < mn_lim);
+        if (vec && full) {
+          r[l] = *reinterpret_cast<const float4 *>(base);
+        } else {
+          float v[4];
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            const bool ok = KC ? (mn < mn_lim && kk + c < k_lim)
+                               : (kk < k_lim && mn + c < mn_lim);
+            v[c] = ok ? base[c] : 0.f;
+          }
+          r[l] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  }
+
+  // Image layout [mn][k], pitch P.
+  template <int P>
+  __device__ static void store(float *__restrict__ s, const float4 (&r)[kLoads]) {
+#pragma unroll
+    for (int l = 0; l < kLoads; l++) {
+      const int idx = threadIdx.x + l * THREADS;
+      if (KC) {
+        const int mn = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
+        *reinterpret_cast<float4 *>(s + mn * P + kq) = r[l];
+      } else {
+        const int kk = idx / (BMN / 4), mn = (idx % (BMN / 4)) * 4;
+        s[(mn + 0) * P + kk] = r[l].x;
+        s[(mn + 1) * P + kk] = r[l].y;
+        s[(mn + 2) * P + kk] = r[l].z;
+        s[(mn + 3) * P + kk] = r[l].w;
+      }
+    }
+  }
+};
+
+template <class C, bool TA, bool TB, bool GUARD>
+__device__ __forceinline__ void sgemm2_body(const GemmArgs &g, float *lds,
+                                            const float *A, const float *B,
+                                            float *Cp, int m0, int n0, bool vec) {
+  using IOA = TileIO2<C::BM, C::BK, C::kThreads, !TA>;
+  using IOB = TileIO2<C::BN, C::BK, C::kThreads, TB>;
+  constexpr int BK = C::BK, P = C::P, TM = C::TM, TN = C::TN;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int arow = wm * (C::BM / C::WM) + lrow;
+  const int brow = wn * (C::BN / C::WN) + lrow;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+
+  float4 ra[IOA::kLoads], rb[IOB::kLoads];
+  const int nk = (g.k + BK - 1) / BK;
+  IOA::template load<GUARD>(A, g.lda, m0, g.m, 0, g.k, vec, ra);
+  IOB::template load<GUARD>(B, g.ldb, n0, g.n, 0, g.k, vec, rb);
+  IOA::template store<P>(lds, ra);
+  IOB::template store<P>(lds + C::BM * P, rb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; kt++) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      IOA::template load<GUARD>(A, g.lda, m0, g.m, (kt + 1) * BK, g.k, vec, ra);
+      IOB::template load<GUARD>(B, g.ldb, n0, g.n, (kt + 1) * BK, g.k, vec, rb);
+    }
+    const float *As = lds + cur * C::kBuf;
+    const float *Bs = As + C::BM * P;
+    float4 fa[TM], fb[TN], na[TM], nb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+      fa[i] = *reinterpret_cast<const float4 *>(As + (arow + 32 * i) * P + 4 * lh);
+#pragma unroll
+    for (int j = 0; j < TN; j++)
+      fb[j] = *reinterpret_cast<const float4 *>(Bs + (brow + 32 * j) * P + 4 * lh);
+#pragma unroll
+    for (int gk = 0; gk < BK / 8; gk++) {
+      if (gk + 1 < BK / 8) {
+        const int ko = 8 * (gk + 1) + 4 * lh;
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+          na[i] = *reinterpret_cast<const float4 *>(As + (arow + 32 * i) * P + ko);
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+          nb[j] = *reinterpret_cast<const float4 *>(Bs + (brow + 32 * j) * P + ko);
+      }
+#pragma unroll
+      for (int sidx = 0; sidx < 4; sidx++)
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+          for (int j = 0; j < TN; j++) {
+            const float av = sidx == 0 ? fa[i].x : sidx == 1 ? fa[i].y : sidx == 2 ? fa[i].z : fa[i].w;
+            const float bv = sidx == 0 ? fb[j].x : sidx == 1 ? fb[j].y : sidx == 2 ? fb[j].z : fb[j].w;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+          }
+      if (gk + 1 < BK / 8) {
+#pragma unroll
+        for (int i = 0; i < TM; i++) fa[i] = na[i];
+#pragma unroll
+        for (int j = 0; j < TN; j++) fb[j] = nb[j];
+      }
+    }
+    if (more) {
+      float *Ad = lds + (cur ^ 1) * C::kBuf;
+      IOA::template store<P>(Ad, ra);
+      IOB::template store<P>(Ad + C::BM * P, rb);
+    }
+    __syncthreads();
+  }
+
+  const bool use_beta = g.beta != 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+      const int col = n0 + brow + j * 32;
+      if (GUARD && col >= g.n) continue;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int row = m0 + arow - lrow + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (!GUARD || row < g.m) {
+          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+          float v = g.alpha * acc[i][j][r];
+          if (use_beta) v += g.beta * *pc;
+          *pc = v;
+        }
+      }
+    }
+}
+
+template <class C, bool TA, bool TB>
+__global__ __launch_bounds__(C::kThreads) void sgemm2_kernel(GemmArgs g, int vec) {
+  __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats];
+  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
+  const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
+  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = static_cast<int>(t / tiles_n) * C::BM;
+  const int n0 = static_cast<int>(t % tiles_n) * C::BN;
+  const float *A = g.a + blockIdx.z * g.stride_a;
+  const float *B = g.b + blockIdx.z * g.stride_b;
+  float *Cp = g.c + blockIdx.z * g.stride_c;
+  const bool interior = vec && m0 + C::BM <= g.m && n0 + C::BN <= g.n &&
+                        g.k % C::BK == 0;
+  if (interior)
+    sgemm2_body<C, TA, TB, false>(g, lds, A, B, Cp, m0, n0, true);
+  else
+    sgemm2_body<C, TA, TB, true>(g, lds, A, B, Cp, m0, n0, vec != 0);
+}
+
+template <class C>
+void launch_cfg2(const GemmArgs &g, int ta, int tb, bool vec, int batch,
+                 hipStream_t s) {
+  const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
+                                               ((g.n + C::BN - 1) / C::BN));
+  const dim3 grid(tiles, 1, static_cast<unsigned>(batch)), block(C::kThreads);
+  const int v = vec ? 1 : 0;
+  if (!ta && !tb)
+    hipLaunchKernelGGL((sgemm2_kernel<C, false, false>), grid, block, 0, s, g, v);
+  else if (!ta && tb)
+    hipLaunchKernelGGL((sgemm2_kernel<C, false, true>), grid, block, 0, s, g, v);
+  else if (ta && !tb)
+    hipLaunchKernelGGL((sgemm2_kernel<C, true, false>), grid, block, 0, s, g, v);
+  else
+    hipLaunchKernelGGL((sgemm2_kernel<C, true, true>), grid, block, 0, s, g, v);
+}
+
 template <class C>
 void launch_cfg(const GemmArgs &g, int ta, int tb, bool vec, int batch,
                 hipStream_t s) {
@@ -247,6 +474,10 @@ using CfgA = Cfg<128, 128, 16, 2, 2>;
 using CfgB = Cfg<128, 128, 32, 2, 2>;
 using CfgC = Cfg<256, 128, 16, 4, 2>;
 using CfgD = Cfg<128, 256, 16, 2, 4>;
+using Cfg2A = Cfg2<128, 128, 32, 2, 2>;
+using Cfg2B = Cfg2<128, 256, 32, 2, 4>;
+using Cfg2C = Cfg2<256, 128, 32, 4, 2>;
+using Cfg2D = Cfg2<128, 128, 64, 2, 2>;
 
 int default_variant() {
   static const int v = [] {
@@ -291,6 +522,10 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
     case 2: launch_cfg<CfgB>(g, ta, tb, vec, batch, s); break;
     case 3: launch_cfg<CfgC>(g, ta, tb, vec, batch, s); break;
     case 4: launch_cfg<CfgD>(g, ta, tb, vec, batch, s); break;
+    case 5: launch_cfg2<Cfg2A>(g, ta, tb, vec, batch, s); break;
+    case 6: launch_cfg2<Cfg2B>(g, ta, tb, vec, batch, s); break;
+    case 7: launch_cfg2<Cfg2C>(g, ta, tb, vec, batch, s); break;
+    case 8: launch_cfg2<Cfg2D>(g, ta, tb, vec, batch, s); break;
     default:
       set_error("vs_sgemm: unknown variant %d", variant);
       return VS_ERR_INVALID;

@@ -143,38 +143,51 @@ __global__ __launch_bounds__(kThreads) void swt_global_kernel(
   lo[blockIdx.y * ls + i] = sl;
 }
 
-// All `levels` stationary levels of one signal in LDS (two ping-pong bands).
-constexpr int kMultiMax = 8192;  // samples per signal held in LDS
+// All `levels` stationary levels of one signal in LDS.  Each level first
+// materialises the boundary extension of the current band behind it (so the
+// tap loop is plain LDS reads with no index arithmetic), then every lane
+// produces outputs i = tid + k * blockDim: the high band goes straight to
+// HBM (coalesced), the low band to the other LDS buffer.
+constexpr int kMultiMax = 8192;   // samples per signal held in LDS
+constexpr int kMultiExt = 4096;   // room for the extension (order-1) 2^(L-1)
 
-__global__ __launch_bounds__(1024) void swt_multi_kernel(
+__global__ __launch_bounds__(256) void swt_multi_kernel(
     Taps taps, int ext, int levels, const float *__restrict__ src, int len,
     float *__restrict__ hi, float *__restrict__ lo) {
-  __shared__ float band[2][kMultiMax];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int stride = len + ((taps.order - 1) << (levels - 1));
+  float *band0 = smem, *band1 = smem + stride;
   const int64_t sig = blockIdx.x;
   const float *x = src + sig * len;
-  for (int i = threadIdx.x; i < len; i += blockDim.x) band[0][i] = x[i];
-  __syncthreads();
-  int cur = 0;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) band0[i] = x[i];
+  float *in = band0, *out = band1;
   for (int l = 0; l < levels; l++) {
     const int dil = 1 << l;
+    const int halo = (taps.order - 1) * dil;
+    __syncthreads();  // band complete
+    for (int t = threadIdx.x; t < halo; t += blockDim.x) {
+      const int j = ext_index(len + t, len, ext);
+      in[len + t] = j < 0 ? 0.f : in[j];
+    }
+    __syncthreads();
     float *hrow = hi + (sig * levels + l) * len;
-    const float *in = band[cur];
-    float *out = band[cur ^ 1];
     for (int i = threadIdx.x; i < len; i += blockDim.x) {
       float sh = 0.f, sl = 0.f;
       for (int r = 0; r < taps.order; r++) {
-        const float v = ext_load(in, i + r * dil, len, ext);
+        const float v = in[i + r * dil];
         sh = fmaf(taps.hp[r], v, sh);
         sl = fmaf(taps.lp[r], v, sl);
       }
       hrow[i] = sh;
       out[i] = sl;
     }
-    __syncthreads();
-    cur ^= 1;
+    float *t = in;
+    in = out;
+    out = t;
   }
+  __syncthreads();
   float *lrow = lo + sig * len;
-  for (int i = threadIdx.x; i < len; i += blockDim.x) lrow[i] = band[cur][i];
+  for (int i = threadIdx.x; i < len; i += blockDim.x) lrow[i] = in[i];
 }
 
 // Mallat pyramid of one signal in LDS: out row = [hi_1 | hi_2 | ... | hi_L | lo_L].
@@ -183,20 +196,25 @@ constexpr int kDwtMultiMax = 16384;
 __global__ __launch_bounds__(1024) void dwt_multi_kernel(
     Taps taps, int ext, int levels, const float *__restrict__ src, int len,
     float *__restrict__ out) {
-  __shared__ float band[kDwtMultiMax + kDwtMultiMax / 2];
+  __shared__ float band[kDwtMultiMax + kMaxOrder + kDwtMultiMax / 2];
   const int64_t sig = blockIdx.x;
   const float *x = src + sig * len;
   float *orow = out + sig * len;
   for (int i = threadIdx.x; i < len; i += blockDim.x) band[i] = x[i];
   __syncthreads();
   int n = len, off = 0;
-  float *in = band, *nxt = band + kDwtMultiMax;
+  float *in = band, *nxt = band + kDwtMultiMax + kMaxOrder;
   for (int l = 0; l < levels; l++) {
     const int half = n / 2;
+    for (int t = threadIdx.x; t < taps.order; t += blockDim.x) {
+      const int j = ext_index(n + t, n, ext);
+      in[n + t] = j < 0 ? 0.f : in[j];
+    }
+    __syncthreads();
     for (int k = threadIdx.x; k < half; k += blockDim.x) {
       float sh = 0.f, sl = 0.f;
       for (int j = 0; j < taps.order; j++) {
-        const float v = ext_load(in, 2 * k + j, n, ext);
+        const float v = in[2 * k + j];
         sh = fmaf(taps.hp[j], v, sh);
         sl = fmaf(taps.lp[j], v, sl);
       }
@@ -303,10 +321,15 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
   Taps t;
   VS_TRY(make_taps(type, order, &t));
   auto s = static_cast<hipStream_t>(stream);
-  if (len <= kMultiMax) {
-    const int threads = len >= 1024 ? 1024 : ((len + 63) / 64) * 64;
+  const long long halo = static_cast<long long>(order - 1) << (levels - 1);
+  if (len <= kMultiMax && halo <= kMultiExt) {
+    const size_t lds = 2 * (static_cast<size_t>(len) + halo) * sizeof(float);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void *>(swt_multi_kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (kMultiMax + kMultiExt) * 4);
+    VS_HIP(attr);
     hipLaunchKernelGGL(swt_multi_kernel, dim3(static_cast<unsigned>(batch)),
-                       dim3(threads), 0, s, t, ext, levels, src, len, hi, lo);
+                       dim3(256), lds, s, t, ext, levels, src, len, hi, lo);
     VS_HIP(hipGetLastError());
     return VS_OK;
   }

@@ -19,11 +19,32 @@ lib.vs_sgemm_variant.argtypes = [ctypes.c_int] * 6 + [ctypes.c_float, ctypes.c_v
                                  ctypes.c_void_p]
 
 
+def check_transposes(variants):
+    """Every variant x (ta, tb) on ragged shapes vs float64 torch."""
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for (m, n, k) in [(300, 1000, 256), (257, 129, 95), (128, 256, 64), (1, 7, 3)]:
+        for ta in (0, 1):
+            for tb in (0, 1):
+                a = torch.rand((k, m) if ta else (m, k), device="cuda") - 0.5
+                b = torch.rand((n, k) if tb else (k, n), device="cuda") - 0.5
+                ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
+                for v in variants:
+                    c = torch.full((m, n), 7.0, device="cuda")
+                    st = lib.vs_sgemm_variant(v, ta, tb, m, n, k, 1.0, a.data_ptr(),
+                                              a.shape[1], b.data_ptr(), b.shape[1], 0.0,
+                                              c.data_ptr(), n, s)
+                    assert st == 0, lib.vs_last_error()
+                    err = (c.double() - ref).abs().max().item()
+                    assert err < 1e-5 * k + 1e-5, (v, ta, tb, m, n, k, err)
+    print("transpose check ok for variants", variants, flush=True)
+
+
 def main():
     shapes = [(4096, 4096, 4096), (8192, 8192, 8192), (2048, 2048, 2048),
               (300, 1000, 256)]
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4").split(",")]
     rounds = int(os.environ.get("ROUNDS", "5"))
+    check_transposes(variants)
     torch.backends.cuda.matmul.allow_tf32 = False
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
