@@ -51,5 +51,22 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
 }
 
+// Output-tile coordinates of linear tile t in GROUP-row bands: consecutive
+// t walk GROUP tile rows down before moving one tile column right, so the
+// blocks an XCD runs together (a contiguous t range after xcd_remap) share
+// ~GROUP A panels and ~(resident / GROUP) B panels in that XCD's L2 instead
+// of 2 A panels and every B panel.
+template <unsigned GROUP = 8>
+__device__ __forceinline__ void grouped_tile(unsigned t, unsigned tiles_m,
+                                             unsigned tiles_n, unsigned &tm,
+                                             unsigned &tn) {
+  const unsigned band = t / (GROUP * tiles_n);
+  const unsigned first = band * GROUP;
+  const unsigned rows = tiles_m - first < GROUP ? tiles_m - first : GROUP;
+  const unsigned in = t - band * GROUP * tiles_n;
+  tm = first + in % rows;
+  tn = in / rows;
+}
+
 }  // namespace dev
 }  // namespace vs

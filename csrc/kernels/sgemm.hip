@@ -65,7 +65,7 @@ struct Cfg {
 // Loads this thread's share of one BK x BMN operand tile into registers.
 //   KCONTIG: operand stored [mn][k] (k contiguous) -> float4 along k.
 //   else   : operand stored [k][mn] (mn contiguous) -> float4 along mn.
-template <int BMN, int BK, int THREADS, bool KCONTIG, bool VEC>
+template <int BMN, int BK, int THREADS, bool KCONTIG, bool VEC, bool INTERIOR = false>
 struct TileIO {
   static constexpr int kLoads = BMN * BK / 4 / THREADS;
   static_assert(kLoads * 4 * THREADS == BMN * BK, "tile not divisible");
@@ -84,6 +84,10 @@ struct TileIO {
         mn = mn0 + (idx % (BMN / 4)) * 4;
       }
       const float *base = KCONTIG ? p + mn * ld + kk : p + kk * ld + mn;
+      if (INTERIOR) {
+        r[l] = *reinterpret_cast<const float4 *>(base);
+        continue;
+      }
       const bool full = KCONTIG ? (mn < mn_lim && kk + 3 < k_lim)
                                 : (kk < k_lim && mn + 3 < mn_lim);
       if (VEC && full) {
@@ -122,19 +126,22 @@ struct TileIO {
 
 // TA / TB: operand stored transposed relative to op().  A is K-contiguous
 // unless TA; B is K-contiguous only if TB.
-template <class C, bool TA, bool TB, bool VEC>
+// INTERIOR (implies VEC): every tile is whole, no load or store is guarded.
+template <class C, bool TA, bool TB, bool VEC, bool INTERIOR = false>
 __global__ __launch_bounds__(C::kThreads) void sgemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats];
-  using IOA = TileIO<C::BM, C::BK, C::kThreads, !TA, VEC>;
-  using IOB = TileIO<C::BN, C::BK, C::kThreads, TB, VEC>;
+  using IOA = TileIO<C::BM, C::BK, C::kThreads, !TA, VEC, INTERIOR>;
+  using IOB = TileIO<C::BN, C::BK, C::kThreads, TB, VEC, INTERIOR>;
   constexpr int BK = C::BK, PA = C::PA, PB = C::PB;
   constexpr int kBuf = BK * (PA + PB);
 
   const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
   const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
   const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = static_cast<int>(t / tiles_n) * C::BM;
-  const int n0 = static_cast<int>(t % tiles_n) * C::BN;
+  unsigned tm, tn;
+  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
+  const int m0 = static_cast<int>(tm) * C::BM;
+  const int n0 = static_cast<int>(tn) * C::BN;
 
   const float *A = g.a + blockIdx.z * g.stride_a;
   const float *B = g.b + blockIdx.z * g.stride_b;
@@ -204,11 +211,11 @@ __global__ __launch_bounds__(C::kThreads) void sgemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < C::TN; j++) {
       const int col = n0 + bn + j * 32;
-      if (col >= g.n) continue;
+      if (!INTERIOR && col >= g.n) continue;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int row = m0 + am - lrow + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (row < g.m) {
+        if (INTERIOR || row < g.m) {
           float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
           float v = g.alpha * acc[i][j][r];
           if (use_beta) v += g.beta * *pc;
@@ -219,36 +226,60 @@ __global__ __launch_bounds__(C::kThreads) void sgemm_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------
-// Generation 2: K-contiguous LDS images + 16-byte fragment reads.
+// Generation 2: natural-layout LDS images, 16-byte global loads AND stores,
+// fragment reads shaped by the operand's layout.
 //
-// Both operand tiles are stored k-contiguous in LDS ([m][k] and [n][k],
-// pitch BK + 4 floats: conflict-free ds_read_b128 for 16 consecutive rows).
-// The 32x32x2 MFMA consumes two k per instruction (lane half h gets one);
-// since the order of the K sum is free, MFMA s (s = 0..3) of an 8-k group
-// takes k = 4h + s, so every lane fetches its 4 k values for 4 MFMAs with
-// ONE ds_read_b128 per operand tile (4x fewer LDS instructions than gen 1).
-// Fragments of group g+1 are read while the MFMAs of group g run, interior
-// tiles use unguarded 16-byte global loads, edge tiles a guarded copy of the
-// same loop (uniform branch per workgroup).
-template <int BM_, int BN_, int BK_, int WM_, int WN_>
+// An operand tile is copied to LDS in the layout it has in memory (no
+// transposing scalar stores -- those were 16-way bank conflicts on the
+// critical path between k-tiles):
+//   K-contiguous ([mn][k], pitch BK + 4):  one ds_read_b128 per lane fetches
+//     the 4 k values of 4 consecutive MFMAs (conflict-free: the 16-lane
+//     groups of ds_read_b128 hit 16 distinct 4-bank groups at pitch BK + 4);
+//   MN-contiguous ([k][mn], pitch BMN + 4): four ds_read_b32, 32 consecutive
+//     columns per half-wave (conflict-free).
+// The 32x32x2 MFMA consumes two k per instruction (lane half h supplies one);
+// the K summation order is free, so MFMA s (s = 0..3) of an 8-k group takes
+// k = 4h + s.  Fragments of group g+1 are read while the MFMAs of group g run;
+// the next k-tile's global loads are issued at the top of the tile and written
+// to the other LDS buffer after group SAT, so their latency is covered by the
+// first groups and the stores by the remaining ones; one barrier per k-tile.
+// Interior tiles run an unguarded copy of the loop (uniform branch per
+// workgroup).
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int SAT_ = -1,
+          int SCHED_ = 0>
 struct Cfg2 {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  // 0: compiler schedule; 1: sched_group_barrier interleave.  (Pinning each
+  // group's MFMAs between sched_barrier(0) fences was measured 25-45 % slower
+  // than either: profiles/r1/sgemm_variants.md.)
+  static constexpr int SCHED = SCHED_;
   static constexpr int kThreads = 64 * WM * WN;
   static constexpr int TM = BM / WM / 32;
   static constexpr int TN = BN / WN / 32;
-  static constexpr int P = BK + 4;  // LDS pitch (floats) of both images
-  static constexpr int kBuf = (BM + BN) * P;
-  static constexpr int kLdsFloats = 2 * kBuf;
+  static constexpr int NG = BK / 8;                    // 8-k groups per tile
+  static constexpr int SAT = SAT_ < 0 ? NG - 1 : SAT_;  // store after group
   static_assert(BK % 8 == 0, "BK must be a multiple of 8");
 };
 
-// Stage one operand tile (BMN rows of the op, BK deep) into registers.
-//   KC: stored [mn][k] (k contiguous)  -> float4 along k, no transpose.
-//   else: stored [k][mn]               -> float4 along mn, transposed on store.
 template <int BMN, int BK, int THREADS, bool KC>
 struct TileIO2 {
   static constexpr int kLoads = BMN * BK / 4 / THREADS;
   static_assert(kLoads * 4 * THREADS == BMN * BK, "tile not divisible");
+  static constexpr int P = KC ? BK + 4 : BMN + 4;      // LDS pitch (floats)
+  static constexpr int kFragReads = KC ? 1 : 4;        // ds_read per frag()
+  static constexpr int kFloats = KC ? BMN * P : BK * P;
+
+  // Thread's (mn, k) coordinates of float4 number l of the tile.
+  __device__ static void coord(int l, int &mn, int &kk) {
+    const int idx = threadIdx.x + l * THREADS;
+    if (KC) {
+      mn = idx / (BK / 4);
+      kk = (idx % (BK / 4)) * 4;
+    } else {
+      kk = idx / (BMN / 4);
+      mn = (idx % (BMN / 4)) * 4;
+    }
+  }
 
   template <bool GUARD>
   __device__ static void load(const float *__restrict__ p, int64_t ld, int mn0,
@@ -256,15 +287,10 @@ struct TileIO2 {
                              float4 (&r)[kLoads]) {
 #pragma unroll
     for (int l = 0; l < kLoads; l++) {
-      const int idx = threadIdx.x + l * THREADS;
       int mn, kk;
-      if (KC) {
-        mn = mn0 + idx / (BK / 4);
-        kk = k0 + (idx % (BK / 4)) * 4;
-      } else {
-        kk = k0 + idx / (BMN / 4);
-        mn = mn0 + (idx % (BMN / 4)) * 4;
-      }
+      coord(l, mn, kk);
+      mn += mn0;
+      kk += k0;
       const float *base = KC ? p + mn * ld + kk : p + kk * ld + mn;
       if (!GUARD) {
         r[l] = *reinterpret_cast<const float4 *>(base);
@@ -287,33 +313,115 @@ struct TileIO2 {
     }
   }
 
-  // Image layout [mn][k], pitch P.
-  template <int P>
   __device__ static void store(float *__restrict__ s, const float4 (&r)[kLoads]) {
 #pragma unroll
     for (int l = 0; l < kLoads; l++) {
-      const int idx = threadIdx.x + l * THREADS;
-      if (KC) {
-        const int mn = idx / (BK / 4), kq = (idx % (BK / 4)) * 4;
-        *reinterpret_cast<float4 *>(s + mn * P + kq) = r[l];
-      } else {
-        const int kk = idx / (BMN / 4), mn = (idx % (BMN / 4)) * 4;
-        s[(mn + 0) * P + kk] = r[l].x;
-        s[(mn + 1) * P + kk] = r[l].y;
-        s[(mn + 2) * P + kk] = r[l].z;
-        s[(mn + 3) * P + kk] = r[l].w;
+      int mn, kk;
+      coord(l, mn, kk);
+      *reinterpret_cast<float4 *>(s + (KC ? mn * P + kk : kk * P + mn)) = r[l];
+    }
+  }
+
+  // The 4 k values (k0 + 0..3) of row/column `mn` of the image.
+  __device__ static float4 frag(const float *__restrict__ s, int mn, int k0) {
+    if (KC) return *reinterpret_cast<const float4 *>(s + mn * P + k0);
+    return make_float4(s[(k0 + 0) * P + mn], s[(k0 + 1) * P + mn],
+                       s[(k0 + 2) * P + mn], s[(k0 + 3) * P + mn]);
+  }
+};
+
+template <class C, bool TA, bool TB>
+struct Layout2 {
+  using IOA = TileIO2<C::BM, C::BK, C::kThreads, !TA>;
+  using IOB = TileIO2<C::BN, C::BK, C::kThreads, TB>;
+  static constexpr int kBuf = IOA::kFloats + IOB::kFloats;
+  static constexpr int kLdsFloats = 2 * kBuf;
+};
+
+__device__ __forceinline__ float comp(const float4 &v, int s) {
+  return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
+}
+
+// One steady-state k-tile (a next tile exists): straight-line code, so the
+// scheduler sees the whole tile as one region and -- with C::SCHED -- the
+// sched_group_barrier sequence at the end pins the interleave: the next
+// tile's global loads first, then every MFMA followed by at most one of the
+// next group's fragment reads (and, after group SAT, the LDS stores).
+template <class C, bool TA, bool TB, bool GUARD, bool MORE>
+__device__ __forceinline__ void ktile(const GemmArgs &g, float *lds,
+                                      const float *A, const float *B, int m0,
+                                      int n0, bool vec, int kt,
+                                      floatx16 (&acc)[C::TM][C::TN],
+                                      float4 (&ra)[Layout2<C, TA, TB>::IOA::kLoads],
+                                      float4 (&rb)[Layout2<C, TA, TB>::IOB::kLoads]) {
+  using L = Layout2<C, TA, TB>;
+  using IOA = typename L::IOA;
+  using IOB = typename L::IOB;
+  constexpr int BK = C::BK, TM = C::TM, TN = C::TN, NG = C::NG;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int arow = wm * (C::BM / C::WM) + lrow;
+  const int brow = wn * (C::BN / C::WN) + lrow;
+  const int cur = kt & 1;
+  if (MORE) {
+    IOA::template load<GUARD>(A, g.lda, m0, g.m, (kt + 1) * BK, g.k, vec, ra);
+    IOB::template load<GUARD>(B, g.ldb, n0, g.n, (kt + 1) * BK, g.k, vec, rb);
+  }
+  const float *As = lds + cur * L::kBuf;
+  const float *Bs = As + IOA::kFloats;
+  float4 fa[NG][TM], fb[NG][TN];
+#pragma unroll
+  for (int gk = 0; gk < NG; gk++) {
+    const int ko = 8 * gk + 4 * lh;
+#pragma unroll
+    for (int i = 0; i < TM; i++) fa[gk][i] = IOA::frag(As, arow + 32 * i, ko);
+#pragma unroll
+    for (int j = 0; j < TN; j++) fb[gk][j] = IOB::frag(Bs, brow + 32 * j, ko);
+#pragma unroll
+    for (int sidx = 0; sidx < 4; sidx++)
+#pragma unroll
+      for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+              comp(fa[gk][i], sidx), comp(fb[gk][j], sidx), acc[i][j], 0, 0, 0);
+    if (MORE && gk == C::SAT) {
+      float *Ad = lds + (cur ^ 1) * L::kBuf;
+      IOA::store(Ad, ra);
+      IOB::store(Ad + IOA::kFloats, rb);
+    }
+  }
+  if constexpr (C::SCHED == 1) {
+    constexpr int kReads = TM * IOA::kFragReads + TN * IOB::kFragReads;
+    constexpr int kMfma = 4 * TM * TN;
+    constexpr int kWrites = IOA::kLoads + IOB::kLoads;
+    if (MORE) __builtin_amdgcn_sched_group_barrier(0x020, IOA::kLoads + IOB::kLoads, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, kReads, 0);  // group 0 fragments
+#pragma unroll
+    for (int gk = 0; gk < NG; gk++) {
+      // MFMAs of group gk, each followed by one read of group gk+1
+#pragma unroll
+      for (int q = 0; q < kMfma; q++) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (gk + 1 < NG && q < kReads) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (MORE && gk == C::SAT && q >= kReads && q < kReads + kWrites)
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
       }
     }
   }
-};
+  __syncthreads();
+}
 
 template <class C, bool TA, bool TB, bool GUARD>
 __device__ __forceinline__ void sgemm2_body(const GemmArgs &g, float *lds,
                                             const float *A, const float *B,
                                             float *Cp, int m0, int n0, bool vec) {
-  using IOA = TileIO2<C::BM, C::BK, C::kThreads, !TA>;
-  using IOB = TileIO2<C::BN, C::BK, C::kThreads, TB>;
-  constexpr int BK = C::BK, P = C::P, TM = C::TM, TN = C::TN;
+  using L = Layout2<C, TA, TB>;
+  using IOA = typename L::IOA;
+  using IOB = typename L::IOB;
+  constexpr int BK = C::BK, TM = C::TM, TN = C::TN, NG = C::NG;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int wm = wid / C::WN, wn = wid % C::WN;
@@ -333,58 +441,56 @@ __device__ __forceinline__ void sgemm2_body(const GemmArgs &g, float *lds,
   const int nk = (g.k + BK - 1) / BK;
   IOA::template load<GUARD>(A, g.lda, m0, g.m, 0, g.k, vec, ra);
   IOB::template load<GUARD>(B, g.ldb, n0, g.n, 0, g.k, vec, rb);
-  IOA::template store<P>(lds, ra);
-  IOB::template store<P>(lds + C::BM * P, rb);
+  IOA::store(lds, ra);
+  IOB::store(lds + IOA::kFloats, rb);
   __syncthreads();
 
   for (int kt = 0; kt < nk; kt++) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
+    if (!GUARD && more) {
+      ktile<C, TA, TB, GUARD, true>(g, lds, A, B, m0, n0, vec, kt, acc, ra, rb);
+      continue;
+    }
     if (more) {
       IOA::template load<GUARD>(A, g.lda, m0, g.m, (kt + 1) * BK, g.k, vec, ra);
       IOB::template load<GUARD>(B, g.ldb, n0, g.n, (kt + 1) * BK, g.k, vec, rb);
     }
-    const float *As = lds + cur * C::kBuf;
-    const float *Bs = As + C::BM * P;
+    const float *As = lds + cur * L::kBuf;
+    const float *Bs = As + IOA::kFloats;
     float4 fa[TM], fb[TN], na[TM], nb[TN];
 #pragma unroll
-    for (int i = 0; i < TM; i++)
-      fa[i] = *reinterpret_cast<const float4 *>(As + (arow + 32 * i) * P + 4 * lh);
+    for (int i = 0; i < TM; i++) fa[i] = IOA::frag(As, arow + 32 * i, 4 * lh);
 #pragma unroll
-    for (int j = 0; j < TN; j++)
-      fb[j] = *reinterpret_cast<const float4 *>(Bs + (brow + 32 * j) * P + 4 * lh);
+    for (int j = 0; j < TN; j++) fb[j] = IOB::frag(Bs, brow + 32 * j, 4 * lh);
 #pragma unroll
-    for (int gk = 0; gk < BK / 8; gk++) {
-      if (gk + 1 < BK / 8) {
+    for (int gk = 0; gk < NG; gk++) {
+      if (gk + 1 < NG) {
         const int ko = 8 * (gk + 1) + 4 * lh;
 #pragma unroll
-        for (int i = 0; i < TM; i++)
-          na[i] = *reinterpret_cast<const float4 *>(As + (arow + 32 * i) * P + ko);
+        for (int i = 0; i < TM; i++) na[i] = IOA::frag(As, arow + 32 * i, ko);
 #pragma unroll
-        for (int j = 0; j < TN; j++)
-          nb[j] = *reinterpret_cast<const float4 *>(Bs + (brow + 32 * j) * P + ko);
+        for (int j = 0; j < TN; j++) nb[j] = IOB::frag(Bs, brow + 32 * j, ko);
       }
 #pragma unroll
       for (int sidx = 0; sidx < 4; sidx++)
 #pragma unroll
         for (int i = 0; i < TM; i++)
 #pragma unroll
-          for (int j = 0; j < TN; j++) {
-            const float av = sidx == 0 ? fa[i].x : sidx == 1 ? fa[i].y : sidx == 2 ? fa[i].z : fa[i].w;
-            const float bv = sidx == 0 ? fb[j].x : sidx == 1 ? fb[j].y : sidx == 2 ? fb[j].z : fb[j].w;
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-          }
-      if (gk + 1 < BK / 8) {
+          for (int j = 0; j < TN; j++)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                comp(fa[i], sidx), comp(fb[j], sidx), acc[i][j], 0, 0, 0);
+      if (gk == C::SAT && more) {
+        float *Ad = lds + (cur ^ 1) * L::kBuf;
+        IOA::store(Ad, ra);
+        IOB::store(Ad + IOA::kFloats, rb);
+      }
+      if (gk + 1 < NG) {
 #pragma unroll
         for (int i = 0; i < TM; i++) fa[i] = na[i];
 #pragma unroll
         for (int j = 0; j < TN; j++) fb[j] = nb[j];
       }
-    }
-    if (more) {
-      float *Ad = lds + (cur ^ 1) * C::kBuf;
-      IOA::template store<P>(Ad, ra);
-      IOB::template store<P>(Ad + C::BM * P, rb);
     }
     __syncthreads();
   }
@@ -409,23 +515,22 @@ __device__ __forceinline__ void sgemm2_body(const GemmArgs &g, float *lds,
     }
 }
 
-template <class C, bool TA, bool TB>
+// INTERIOR: the launcher checked that every tile is whole and 16-byte
+// aligned; that instance carries no guarded code at all.
+template <class C, bool TA, bool TB, bool INTERIOR>
 __global__ __launch_bounds__(C::kThreads) void sgemm2_kernel(GemmArgs g, int vec) {
-  __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats];
+  __shared__ __attribute__((aligned(16))) float lds[Layout2<C, TA, TB>::kLdsFloats];
   const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
   const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
   const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = static_cast<int>(t / tiles_n) * C::BM;
-  const int n0 = static_cast<int>(t % tiles_n) * C::BN;
+  unsigned tm, tn;
+  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
+  const int m0 = static_cast<int>(tm) * C::BM;
+  const int n0 = static_cast<int>(tn) * C::BN;
   const float *A = g.a + blockIdx.z * g.stride_a;
   const float *B = g.b + blockIdx.z * g.stride_b;
   float *Cp = g.c + blockIdx.z * g.stride_c;
-  const bool interior = vec && m0 + C::BM <= g.m && n0 + C::BN <= g.n &&
-                        g.k % C::BK == 0;
-  if (interior)
-    sgemm2_body<C, TA, TB, false>(g, lds, A, B, Cp, m0, n0, true);
-  else
-    sgemm2_body<C, TA, TB, true>(g, lds, A, B, Cp, m0, n0, vec != 0);
+  sgemm2_body<C, TA, TB, !INTERIOR>(g, lds, A, B, Cp, m0, n0, vec != 0);
 }
 
 template <class C>
@@ -434,15 +539,23 @@ void launch_cfg2(const GemmArgs &g, int ta, int tb, bool vec, int batch,
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
   const dim3 grid(tiles, 1, static_cast<unsigned>(batch)), block(C::kThreads);
+  const bool aligned = vec && g.m % C::BM == 0 && g.n % C::BN == 0 && g.k % C::BK == 0;
   const int v = vec ? 1 : 0;
-  if (!ta && !tb)
-    hipLaunchKernelGGL((sgemm2_kernel<C, false, false>), grid, block, 0, s, g, v);
-  else if (!ta && tb)
-    hipLaunchKernelGGL((sgemm2_kernel<C, false, true>), grid, block, 0, s, g, v);
-  else if (ta && !tb)
-    hipLaunchKernelGGL((sgemm2_kernel<C, true, false>), grid, block, 0, s, g, v);
-  else
-    hipLaunchKernelGGL((sgemm2_kernel<C, true, true>), grid, block, 0, s, g, v);
+#define VS_LAUNCH2(TA_, TB_)                                                        \
+  if (aligned)                                                                      \
+    hipLaunchKernelGGL((sgemm2_kernel<C, TA_, TB_, true>), grid, block, 0, s, g, v); \
+  else                                                                              \
+    hipLaunchKernelGGL((sgemm2_kernel<C, TA_, TB_, false>), grid, block, 0, s, g, v);
+  if (!ta && !tb) {
+    VS_LAUNCH2(false, false)
+  } else if (!ta && tb) {
+    VS_LAUNCH2(false, true)
+  } else if (ta && !tb) {
+    VS_LAUNCH2(true, false)
+  } else {
+    VS_LAUNCH2(true, true)
+  }
+#undef VS_LAUNCH2
 }
 
 template <class C>
@@ -451,8 +564,11 @@ void launch_cfg(const GemmArgs &g, int ta, int tb, bool vec, int batch,
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
   const dim3 grid(tiles, 1, static_cast<unsigned>(batch)), block(C::kThreads);
+  const bool interior = vec && g.m % C::BM == 0 && g.n % C::BN == 0 && g.k % C::BK == 0;
 #define VS_L(TA_, TB_)                                                       \
-  if (vec)                                                                   \
+  if (interior)                                                              \
+    hipLaunchKernelGGL((sgemm_kernel<C, TA_, TB_, true, true>), grid, block, 0, s, g); \
+  else if (vec)                                                              \
     hipLaunchKernelGGL((sgemm_kernel<C, TA_, TB_, true>), grid, block, 0, s, g); \
   else                                                                       \
     hipLaunchKernelGGL((sgemm_kernel<C, TA_, TB_, false>), grid, block, 0, s, g);
@@ -474,10 +590,9 @@ using CfgA = Cfg<128, 128, 16, 2, 2>;
 using CfgB = Cfg<128, 128, 32, 2, 2>;
 using CfgC = Cfg<256, 128, 16, 4, 2>;
 using CfgD = Cfg<128, 256, 16, 2, 4>;
-using Cfg2A = Cfg2<128, 128, 32, 2, 2>;
-using Cfg2B = Cfg2<128, 256, 32, 2, 4>;
-using Cfg2C = Cfg2<256, 128, 32, 4, 2>;
-using Cfg2D = Cfg2<128, 128, 64, 2, 2>;
+using Cfg2A = Cfg2<128, 128, 32, 2, 2, 1, 1>;
+using Cfg2B = Cfg2<256, 128, 32, 4, 2, 1, 1>;
+using Cfg2C = Cfg2<128, 256, 32, 2, 4, 1, 1>;
 
 int default_variant() {
   static const int v = [] {
@@ -508,13 +623,13 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
                    (batch == 1 || (sa % 4 == 0 && sb % 4 == 0));
   if (variant < 0) variant = default_variant();
   if (variant < 0) {
-    // Few 128x128 tiles cannot fill 256 CUs: use 64x64 tiles then.
     // Largest tile that still gives every CU work (A/B on MI355X,
-    // profiles/r1/sgemm_variants.json): 128x256 when >= 512 tiles,
-    // 128x128 when >= 256, else 64x64.
+    // profiles/r1/sgemm_variants.md): 256x128 (gen 1, BK 16) when >= 512
+    // tiles, 128x128 (gen 2, BK 32, interleaved schedule) when >= 256, else
+    // 64x64.
     const long t128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
-    const long t256 = static_cast<long>((m + 127) / 128) * ((n + 255) / 256) * batch;
-    variant = t256 >= 512 ? 4 : (t128 >= 256 ? 1 : 0);
+    const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
+    variant = t256 >= 512 ? 3 : (t128 >= 256 ? 5 : 0);
   }
   switch (variant) {
     case 0: launch_cfg<CfgSmall>(g, ta, tb, vec, batch, s); break;
@@ -525,7 +640,6 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
     case 5: launch_cfg2<Cfg2A>(g, ta, tb, vec, batch, s); break;
     case 6: launch_cfg2<Cfg2B>(g, ta, tb, vec, batch, s); break;
     case 7: launch_cfg2<Cfg2C>(g, ta, tb, vec, batch, s); break;
-    case 8: launch_cfg2<Cfg2D>(g, ta, tb, vec, batch, s); break;
     default:
       set_error("vs_sgemm: unknown variant %d", variant);
       return VS_ERR_INVALID;
@@ -556,7 +670,7 @@ vs_status vs_sgemm_strided_batched(int ta, int tb, int m, int n, int k,
                         beta, c, ldc, sc, batch, static_cast<hipStream_t>(stream));
 }
 
-// Tuning entry point: run one explicit tile variant (0..4).
+// Tuning entry point: run one explicit tile variant (0..7).
 vs_status vs_sgemm_variant(int variant, int ta, int tb, int m, int n, int k,
                            float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,
