@@ -32,7 +32,9 @@ typedef enum {
   VS_ERR_HIP = 2,          ///< HIP runtime error
   VS_ERR_NO_GPU = 3,       ///< no usable gfx950 device
   VS_ERR_UNSUPPORTED = 4,  ///< shape/parameter outside what is implemented
-  VS_ERR_ALLOC = 5         ///< allocation failure
+  VS_ERR_ALLOC = 5,        ///< allocation failure
+  VS_ERR_COMM = 6,         ///< RCCL error (communicator aborted)
+  VS_ERR_TIMEOUT = 7       ///< distributed wait exceeded its timeout
 } vs_status;
 
 typedef enum {

@@ -1,0 +1,178 @@
+"""Native multi-GPU layer (csrc/dist/dist.cpp) -- SURVEY.md §2.2 rows D2-D5.
+
+CPU: the shard arithmetic and the no-GPU error path.  GPU: every collective
+and sharded entry point with the LOCAL backend at 1-4 virtual ranks sharing
+one MI355X (the in-process fake communicator of SURVEY.md §4 item 4), plus the
+RCCL backend over the devices present (one rank per device).  Oracles: numpy
+float64 and the single-device host reference (`*_na`) of the same op.
+"""
+import numpy as np
+import pytest
+
+from veles.simd_amd import _lib, capi
+from veles.simd_amd.parallel import native
+
+pytestmark = pytest.mark.skipif(not _lib.available(), reason="native library not built")
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (7, 8), (0, 2), (1 << 20, 8), (5, 1)])
+def test_shard_covers_range(n, world):
+    spans = [native.shard(n, world, r) for r in range(world)]
+    assert spans[0][0] == 0
+    for (b0, c0), (b1, _) in zip(spans, spans[1:]):
+        assert b0 + c0 == b1
+    assert sum(c for _, c in spans) == n
+    counts = [c for _, c in spans]
+    assert max(counts) - min(counts) <= 1
+    assert counts == sorted(counts, reverse=True)
+
+
+def test_shard_bad_rank():
+    assert native.shard(10, 2, 5) == (0, 0)
+
+
+def test_create_without_gpu_fails_loudly():
+    if _lib.gpu_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.VelesError, match="status 3"):
+        native.DeviceGroup(2, backend="local")
+
+
+# ------------------------------------------------------------------ GPU
+WORLDS = [1, 2, 3, 4]
+
+
+def _group(world, backend="local"):
+    return native.DeviceGroup(world, devices=[0] * world if backend == "local" else None,
+                              backend=backend, timeout_ms=120000)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", WORLDS)
+def test_local_collectives(world):
+    import torch
+    with _group(world) as g:
+        assert g.size == world and g.backend == ("local" if world > 1 else "local")
+        n = 1000
+        bufs = [torch.full((n,), float(r + 1), device="cuda") for r in range(world)]
+        g.broadcast(bufs, root=world - 1)
+        for b in bufs:
+            assert torch.all(b == world)
+        send = [torch.arange(n, device="cuda", dtype=torch.float32) + 1000 * r
+                for r in range(world)]
+        recv = [torch.empty(world * n, device="cuda") for _ in range(world)]
+        g.all_gather(send, recv)
+        want = torch.cat(send)
+        for r in recv:
+            assert torch.equal(r, want)
+        red = [torch.full((n,), float(r), device="cuda") for r in range(world)]
+        g.all_reduce_sum(red)
+        for r in red:
+            assert torch.all(r == sum(range(world)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("direction", [1, -1])
+@pytest.mark.parametrize("periodic", [False, True])
+def test_local_halo(world, direction, periodic):
+    import torch
+    h = 5
+    with _group(world) as g:
+        src = [torch.arange(10 + r, device="cuda", dtype=torch.float32) + 100 * r
+               for r in range(world)]
+        halo = [torch.full((h,), -1.0, device="cuda") for _ in range(world)]
+        g.halo_exchange(src, halo, direction=direction, periodic=periodic)
+        for r in range(world):
+            q = r - 1 if direction > 0 else r + 1
+            if q < 0 or q >= world:
+                if not periodic:
+                    assert torch.all(halo[r] == 0)
+                    continue
+                q %= world
+            want = src[q][-h:] if direction > 0 else src[q][:h]
+            assert torch.equal(halo[r], want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sgemm_rowsplit(world):
+    rng = np.random.default_rng(world)
+    a = rng.standard_normal((3, 131, 70)).astype(np.float32)
+    b = rng.standard_normal((3, 70, 45)).astype(np.float32)
+    with _group(world) as g:
+        c = g.sgemm_rowsplit(a, b)
+    ref = a.astype(np.float64) @ b.astype(np.float64)
+    np.testing.assert_allclose(c, ref, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 3])
+@pytest.mark.parametrize("correlate", [False, True])
+def test_conv1d_batch(world, correlate):
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((5, 3000)).astype(np.float32)
+    h = rng.standard_normal(77).astype(np.float32)
+    with _group(world) as g:
+        y = g.conv1d_batch(x, h, correlate=correlate)
+    hh = h[::-1] if correlate else h
+    ref = np.stack([np.convolve(r.astype(np.float64), hh.astype(np.float64)) for r in x])
+    np.testing.assert_allclose(y, ref, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("correlate", [False, True])
+@pytest.mark.parametrize("hlen", [1, 50, 1024])
+def test_conv1d_long(world, correlate, hlen):
+    rng = np.random.default_rng(hlen)
+    x = rng.standard_normal(20011).astype(np.float32)
+    h = rng.standard_normal(hlen).astype(np.float32)
+    with _group(world) as g:
+        y = g.conv1d_long(x, h, correlate=correlate)
+    hh = h[::-1] if correlate else h
+    ref = np.convolve(x.astype(np.float64), hh.astype(np.float64))
+    np.testing.assert_allclose(y, ref, atol=5e-3 * max(1.0, np.sqrt(hlen) / 8))
+
+
+@pytest.mark.gpu
+def test_conv1d_long_rejects_short_chunks():
+    with _group(4) as g, pytest.raises(_lib.VelesError, match="shorter than the filter"):
+        g.conv1d_long(np.ones(100, np.float32), np.ones(64, np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("ext", ["periodic", "mirror", "constant", "zero"])
+def test_swt_long(world, ext):
+    x = (np.sin(np.arange(4096) * 0.37) * 100).astype(np.float32)
+    levels, order = 3, 8
+    with _group(world) as g:
+        hi, lo = g.swt_long(x, "daubechies", order, levels, ext)
+    cur = x
+    for lvl in range(1, levels + 1):
+        rh, rl = capi.stationary_wavelet_apply(0, order, lvl, native.EXTENSIONS[ext], cur,
+                                               na=True)
+        np.testing.assert_allclose(hi[lvl - 1], rh, atol=5e-2, rtol=1e-4)
+        cur = rl
+    np.testing.assert_allclose(lo, cur, atol=5e-2, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_rccl_backend_one_rank_per_device():
+    """RCCL communicator over the devices present (1 on the test box)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    with native.DeviceGroup(ndev, backend="rccl", timeout_ms=120000) as g:
+        assert g.backend == "rccl"
+        bufs = [torch.full((256,), float(r), device=f"cuda:{r}") for r in range(ndev)]
+        g.all_reduce_sum(bufs)
+        for b in bufs:
+            assert torch.all(b.cpu() == sum(range(ndev)))
+        x = np.random.default_rng(0).standard_normal(50000).astype(np.float32)
+        h = np.ones(33, np.float32)
+        y = g.conv1d_long(x, h)
+        np.testing.assert_allclose(y, np.convolve(x, h), atol=2e-3)
+        a = np.random.default_rng(1).standard_normal((2, 64, 32)).astype(np.float32)
+        b = np.random.default_rng(2).standard_normal((2, 32, 48)).astype(np.float32)
+        np.testing.assert_allclose(g.sgemm_rowsplit(a, b), a @ b, atol=1e-3)

@@ -71,6 +71,24 @@ _SIGNATURES = {
     "vs_dwt_multilevel": (_i, [_i, _i, _i, _i, _vp, _i, _vp, _i, _vp]),
     "vs_wavelet_filter": (_i, [_i, _i, _vp]),
     "vs_detect_peaks": (_i, [_vp, _sz, _i, _vp, _vp, _sz, _vp, _vp]),
+    # multi-GPU layer (include/simd/dist.h)
+    "vs_dist_create": (_i, [_i, _vp, _i, ctypes.POINTER(_vp)]),
+    "vs_dist_destroy": (_i, [_vp]),
+    "vs_dist_size": (_i, [_vp]),
+    "vs_dist_backend_of": (_i, [_vp]),
+    "vs_dist_device": (_i, [_vp, _i]),
+    "vs_dist_stream": (_vp, [_vp, _i]),
+    "vs_dist_set_timeout": (_i, [_vp, _i]),
+    "vs_dist_synchronize": (_i, [_vp]),
+    "vs_dist_shard": (None, [_sz, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
+    "vs_dist_broadcast": (_i, [_vp, _vp, _sz, _i]),
+    "vs_dist_all_gather": (_i, [_vp, _vp, _vp, _sz]),
+    "vs_dist_all_reduce_sum": (_i, [_vp, _vp, _sz]),
+    "vs_dist_halo_exchange": (_i, [_vp, _vp, _vp, _vp, _sz, _i, _i]),
+    "vs_dist_sgemm_rowsplit": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i]),
+    "vs_dist_conv1d_batch": (_i, [_vp, _i, _vp, _i, _vp, _i, _vp, _i]),
+    "vs_dist_conv1d_long": (_i, [_vp, _i, _vp, _sz, _vp, _i, _vp]),
+    "vs_dist_swt_long": (_i, [_vp, _i, _i, _i, _i, _vp, _sz, _vp, _vp]),
 }
 
 _lock = threading.Lock()
