@@ -147,10 +147,23 @@ ConvolutionHandle auto_init(size_t xl, size_t hl, int reverse) {
   return h;
 }
 
+// Direct convolutions below this many multiply-adds run the host reference
+// even with simd = 1 when every operand is in host memory: a GPU round trip
+// (stage in, launch, stage out, sync) costs ~40 us on MI355X, the host loop
+// ~0.3 ns per MAC (profiles/r1/reference_shapes.json).  VELES_HOST_MAX_MACS.
+size_t host_max_macs() {
+  static const size_t v = [] {
+    const char *e = std::getenv("VELES_HOST_MAX_MACS");
+    return e && *e ? static_cast<size_t>(std::atoll(e)) : static_cast<size_t>(1) << 17;
+  }();
+  return v;
+}
+
 void direct(const char *what, int simd, int reverse, const float *x, size_t xl,
             const float *h, size_t hl, float *result) {
   if (!x || !h || !result || !xl || !hl) vs::fatal("%s: invalid arguments", what);
-  if (vs::api::use_gpu_simd(simd, what)) {
+  const bool tiny = xl * hl < host_max_macs() && !vs::api::any_device({x, h, result});
+  if (!tiny && vs::api::use_gpu_simd(simd, what)) {
     gpu_conv(what, VS_CONV_DIRECT, reverse, x, xl, h, hl, result);
   } else if (reverse) {
     vs::ref::correlate_direct(x, xl, h, hl, result);

@@ -79,7 +79,9 @@ void wavelet_apply(WaveletType type, int order, ExtensionType ext,
                    float *destlo) {
   check_dwt_args("wavelet_apply", type, order, ext, src, length, desthi, destlo);
   if (length % 2) vs::fatal("wavelet_apply: odd length %zu", length);
-  if (!vs::gpu_available()) {
+  // Flag-less API (like arithmetic.h): GPU for device operands or enough
+  // work (length x taps) to amortise the host<->device round trip.
+  if (!vs::api::use_gpu_array(length * order, {src, desthi, destlo})) {
     vs::ref::dwt(type, order, ext, src, length, desthi, destlo);
     return;
   }
@@ -112,7 +114,7 @@ void stationary_wavelet_apply(WaveletType type, int order, int level,
   check_dwt_args("stationary_wavelet_apply", type, order, ext, src, length,
                  desthi, destlo);
   if (level < 1) vs::fatal("stationary_wavelet_apply: level %d < 1", level);
-  if (!vs::gpu_available()) {
+  if (!vs::api::use_gpu_array(length * order, {src, desthi, destlo})) {
     vs::ref::swt(type, order, level, ext, src, length, desthi, destlo);
     return;
   }

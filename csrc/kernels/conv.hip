@@ -439,11 +439,14 @@ vs_status vs_conv1d(int algo, int correlate, const float *x, int xlen,
   VS_REQUIRE(batch <= 1 || (xs >= xlen && ys >= ylen),
              "vs_conv1d: row strides smaller than the rows");
   VS_REQUIRE(hs == 0 || hs >= hlen, "vs_conv1d: filter stride < filter length");
-  VS_REQUIRE(batch <= 65535 || algo == VS_CONV_OVERLAP_SAVE,
-             "vs_conv1d: batch > 65535");
   if (batch == 0) return VS_OK;
   auto s = static_cast<hipStream_t>(stream);
   if (algo == VS_CONV_AUTO) algo = conv::select(xlen, hlen, batch);
+  if (batch > kMaxGridY && algo != VS_CONV_OVERLAP_SAVE)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_conv1d(algo, correlate, x + b0 * xs, xlen, xs, h + b0 * hs, hlen, hs,
+                       y + b0 * ys, ys, nb, stream);
+    });
   log(2, "vs_conv1d: x=%d h=%d batch=%d algo=%d", xlen, hlen, batch, algo);
   switch (algo) {
     case VS_CONV_DIRECT:

@@ -379,7 +379,11 @@ vs_status vs_fft_c2c(const float *in, float *out, int n, int batch, int inverse,
   VS_REQUIRE(in && out, "vs_fft_c2c: null pointer");
   VS_REQUIRE(logn >= 1 && logn <= fft::kMaxLog,
              "vs_fft_c2c: n = %d must be a power of two in [2, 2^24]", n);
-  VS_REQUIRE(batch >= 0 && batch <= 65535, "vs_fft_c2c: batch out of range");
+  VS_REQUIRE(batch >= 0, "vs_fft_c2c: negative batch");
+  if (batch > kMaxGridY)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_fft_c2c(in + b0 * 2 * n, out + b0 * 2 * n, n, nb, inverse, stream);
+    });
   return fft::c2c(logn, inverse != 0, reinterpret_cast<const float2 *>(in),
                   reinterpret_cast<float2 *>(out), batch,
                   static_cast<hipStream_t>(stream));
@@ -392,6 +396,10 @@ vs_status vs_fft_r2c(const float *in, float *out, int n, int batch,
   VS_REQUIRE(logn >= 2 && logn <= fft::kMaxLog + 1,
              "vs_fft_r2c: n = %d must be a power of two in [4, 2^25]", n);
   if (batch <= 0) return VS_OK;
+  if (batch > kMaxGridY)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_fft_r2c(in + b0 * n, out + b0 * (n + 2), n, nb, stream);
+    });
   auto s = static_cast<hipStream_t>(stream);
   const int logh = logn - 1, h = n / 2;
   DeviceBuffer z;
@@ -416,6 +424,10 @@ vs_status vs_fft_c2r(const float *in, float *out, int n, int batch,
   VS_REQUIRE(logn >= 2 && logn <= fft::kMaxLog + 1,
              "vs_fft_c2r: n = %d must be a power of two in [4, 2^25]", n);
   if (batch <= 0) return VS_OK;
+  if (batch > kMaxGridY)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_fft_c2r(in + b0 * (n + 2), out + b0 * n, n, nb, stream);
+    });
   auto s = static_cast<hipStream_t>(stream);
   const int logh = logn - 1, h = n / 2;
   DeviceBuffer z;

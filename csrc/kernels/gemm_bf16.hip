@@ -1,0 +1,432 @@
+// bf16 matrix-core GEMM and the "bf16x3" fast-fp32 mode (SURVEY.md §2.3 K8:
+// "optional bf16x3 / bf16 MFMA modes"; build plan §7.2 step 4).
+//
+//   vs_gemm_bf16:   C(fp32) = alpha op(A) op(B) + beta C, A/B bf16.
+//   vs_sgemm_ex(VS_GEMM_BF16X3, ...): fp32 operands split as x = hi + lo
+//     (hi = bf16(x), lo = bf16(x - hi)); C = hi_a hi_b + hi_a lo_b + lo_a hi_b
+//     accumulated in fp32 by v_mfma_f32_32x32x16_bf16.  The dropped lo*lo
+//     term and the 16-bit split leave ~2^-16 relative error per product
+//     (vs 2^-24 for exact fp32) at 3 bf16 MFMAs (3 x 32 cycles per 32x32x16
+//     block) instead of 8 f32 MFMAs (8 x 64 cycles) -- a 5x shorter MFMA
+//     critical path.
+//
+// Structure: a prepass (split_kernel / pack_kernel) writes every operand as
+// a zero-padded, K-contiguous bf16 image ([Mp][Kp] for A, [Np][Kp] for B,
+// transposing B when it is stored [k][n]), so the main kernel has no edge
+// cases, only 16-byte loads and one layout.  Main kernel (template
+// <TERMS, BM, BN, WM, WN>, BK = 32): LDS images [rows][BK + 8] bf16 (80-byte
+// rows: the 16-lane groups of ds_read_b128 hit 16 distinct 4-bank groups),
+// two buffers, register-staged prefetch of tile t+1 during the MFMAs of tile
+// t, one barrier per k-tile; lane l of a 32x32x16 MFMA reads row l & 31,
+// k = 8 (l >> 5) .. +7 of both images with one ds_read_b128 each.  XCD-aware
+// grouped tile order as in sgemm.hip.
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "csrc/kernels/device.h"
+#include "csrc/runtime/runtime.h"
+#include "simd/gpu.h"
+
+namespace vs {
+namespace gbf {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kBK = 32;   // k per LDS tile
+constexpr int kPad = 8;   // bf16 elements of row padding (16 bytes)
+constexpr int kP = kBK + kPad;
+
+__device__ __forceinline__ uint16_t bf16_bits(float x) {
+  const __bf16 h = static_cast<__bf16>(x);
+  return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float bf16_float(uint16_t b) {
+  return __uint_as_float(static_cast<uint32_t>(b) << 16);
+}
+
+// ---------------------------------------------------------------- prepass
+// dst[r][c] (r < rows_p, c < cols_p, row stride cols_p) from the logical
+// operand element (r, c) = src[r * ld + c] (TRANS = 0) or src[c * ld + r]
+// (TRANS = 1), zero outside rows x cols.  SPLIT: fp32 source, writes hi and
+// lo images; else bf16 source (uint16 bits), one image.  32x32 tiles through
+// LDS so both the global read and the write are coalesced when transposing.
+template <bool SPLIT, bool TRANS>
+__global__ __launch_bounds__(256) void pack_kernel(const void *__restrict__ src,
+                                                   int64_t ld, int rows, int cols,
+                                                   int rows_p, int cols_p,
+                                                   uint16_t *__restrict__ hi,
+                                                   uint16_t *__restrict__ lo,
+                                                   int64_t sstride, int64_t dstride) {
+  __shared__ float tile[32][33];
+  const int tr = threadIdx.x >> 5, tc = threadIdx.x & 31;  // 8 x 32
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const float *sf = static_cast<const float *>(src) + blockIdx.z * sstride;
+  const uint16_t *sh = static_cast<const uint16_t *>(src) + blockIdx.z * sstride;
+  auto fetch = [&](int r, int c) -> float {
+    if (r >= rows || c >= cols) return 0.f;
+    const int64_t off = TRANS ? static_cast<int64_t>(c) * ld + r
+                              : static_cast<int64_t>(r) * ld + c;
+    return SPLIT ? sf[off] : bf16_float(sh[off]);
+  };
+  if (TRANS) {
+    // read along r (contiguous in memory), write transposed through LDS
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) tile[tc][tr + i] = fetch(r0 + tc, c0 + tr + i);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+      const int r = r0 + tr + i, c = c0 + tc;
+      const float v = tile[tr + i][tc];
+      if (r < rows_p && c < cols_p) {
+        const int64_t o = blockIdx.z * dstride + static_cast<int64_t>(r) * cols_p + c;
+        const uint16_t h = bf16_bits(v);
+        hi[o] = h;
+        if (SPLIT) lo[o] = bf16_bits(v - bf16_float(h));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+      const int r = r0 + tr + i, c = c0 + tc;
+      if (r < rows_p && c < cols_p) {
+        const float v = fetch(r, c);
+        const int64_t o = blockIdx.z * dstride + static_cast<int64_t>(r) * cols_p + c;
+        const uint16_t h = bf16_bits(v);
+        hi[o] = h;
+        if (SPLIT) lo[o] = bf16_bits(v - bf16_float(h));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ main kernel
+struct Args {
+  const uint16_t *a[2];  // [Mp][Kp] images: hi (and lo)
+  const uint16_t *b[2];  // [Np][Kp]
+  int64_t sa, sb;        // batch strides of the images (elements)
+  int kp;
+  int m, n;              // logical output size
+  float alpha, beta;
+  float *c;
+  int64_t ldc, sc;
+};
+
+template <int TERMS_, int BM_, int BN_, int WM_, int WN_>
+struct Cfg {
+  static constexpr int TERMS = TERMS_, BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int NIMG = TERMS == 1 ? 1 : 2;  // images per operand
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static constexpr int kImgA = BM * kP, kImgB = BN * kP;      // bf16 elements
+  static constexpr int kStage = NIMG * (kImgA + kImgB);
+  static constexpr int kLdsBytes = 2 * kStage * 2;
+  // 16-byte chunks per image per k-tile and per thread
+  static constexpr int kLoadsA = BM * kBK / 8 / kThreads;
+  static constexpr int kLoadsB = BN * kBK / 8 / kThreads;
+  static_assert(kLoadsA * 8 * kThreads == BM * kBK, "A tile split");
+  static_assert(kLoadsB * 8 * kThreads == BN * kBK, "B tile split");
+};
+
+template <int ROWS, int THREADS, int LOADS>
+struct Stage {
+  __device__ static void load(const uint16_t *__restrict__ img, int64_t kp, int row0,
+                              int k0, uint4 (&r)[LOADS]) {
+#pragma unroll
+    for (int l = 0; l < LOADS; l++) {
+      const int idx = threadIdx.x + l * THREADS;
+      const int row = idx / (kBK / 8), kc = (idx % (kBK / 8)) * 8;
+      r[l] = *reinterpret_cast<const uint4 *>(img + (row0 + row) * kp + k0 + kc);
+    }
+  }
+  __device__ static void store(uint16_t *__restrict__ s, const uint4 (&r)[LOADS]) {
+#pragma unroll
+    for (int l = 0; l < LOADS; l++) {
+      const int idx = threadIdx.x + l * THREADS;
+      const int row = idx / (kBK / 8), kc = (idx % (kBK / 8)) * 8;
+      *reinterpret_cast<uint4 *>(s + row * kP + kc) = r[l];
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x8 frag(const uint16_t *s, int row, int k) {
+  return *reinterpret_cast<const bf16x8 *>(s + row * kP + k);
+}
+
+template <class C>
+__global__ __launch_bounds__(C::kThreads) void gemm_kernel(Args g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  using SA = Stage<C::BM, C::kThreads, C::kLoadsA>;
+  using SB = Stage<C::BN, C::kThreads, C::kLoadsB>;
+  constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
+
+  const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
+  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
+  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  unsigned tm, tn;
+  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
+  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
+  const int64_t kp = g.kp;
+
+  const uint16_t *A[2], *B[2];
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    A[i] = g.a[i] + blockIdx.z * g.sa;
+    B[i] = g.b[i] + blockIdx.z * g.sb;
+  }
+  float *Cp = g.c + blockIdx.z * g.sc;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int arow = wm * (C::BM / C::WM) + lrow;
+  const int brow = wn * (C::BN / C::WN) + lrow;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+
+  uint4 ra[NI][C::kLoadsA], rb[NI][C::kLoadsB];
+  auto img_a = [&](int buf, int i) { return lds + buf * C::kStage + i * C::kImgA; };
+  auto img_b = [&](int buf, int i) {
+    return lds + buf * C::kStage + NI * C::kImgA + i * C::kImgB;
+  };
+  const int nk = g.kp / kBK;
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    SA::load(A[i], kp, m0, 0, ra[i]);
+    SB::load(B[i], kp, n0, 0, rb[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    SA::store(img_a(0, i), ra[i]);
+    SB::store(img_b(0, i), rb[i]);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; kt++) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < NI; i++) {
+        SA::load(A[i], kp, m0, (kt + 1) * kBK, ra[i]);
+        SB::load(B[i], kp, n0, (kt + 1) * kBK, rb[i]);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < kBK / 16; ks++) {
+      const int ko = ks * 16 + 8 * lh;
+      bf16x8 fa[NI][TM], fb[NI][TN];
+#pragma unroll
+      for (int i = 0; i < NI; i++) {
+#pragma unroll
+        for (int x = 0; x < TM; x++) fa[i][x] = frag(img_a(cur, i), arow + 32 * x, ko);
+#pragma unroll
+        for (int y = 0; y < TN; y++) fb[i][y] = frag(img_b(cur, i), brow + 32 * y, ko);
+      }
+#pragma unroll
+      for (int x = 0; x < TM; x++)
+#pragma unroll
+        for (int y = 0; y < TN; y++) {
+          // small terms first, so the big one is added last
+          if (C::TERMS == 3) {
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][x], fb[0][y],
+                                                                acc[x][y], 0, 0, 0);
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[1][y],
+                                                                acc[x][y], 0, 0, 0);
+          }
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[0][y],
+                                                              acc[x][y], 0, 0, 0);
+        }
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < NI; i++) {
+        SA::store(img_a(cur ^ 1, i), ra[i]);
+        SB::store(img_b(cur ^ 1, i), rb[i]);
+      }
+    }
+    __syncthreads();
+  }
+
+  const bool use_beta = g.beta != 0.f;
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      const int col = n0 + brow + 32 * y;
+      if (col >= g.n) continue;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int row = m0 + arow - lrow + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < g.m) {
+          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+          float v = g.alpha * acc[x][y][r];
+          if (use_beta) v += g.beta * *pc;
+          *pc = v;
+        }
+      }
+    }
+}
+
+template <class C>
+vs_status launch(const Args &g, int batch, hipStream_t s) {
+  // per launch: the attribute is per device and the call is cheap
+  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_kernel<C>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes));
+  const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
+                                               ((g.n + C::BN - 1) / C::BN));
+  hipLaunchKernelGGL(gemm_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
+                     dim3(C::kThreads), C::kLdsBytes, s, g);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+// Pack one operand.  rows x cols is the logical op(X) with rows along the
+// output (M or N) and cols along K; `trans` = element (r, c) at src[c*ld + r].
+vs_status pack(bool split, bool trans, const void *src, int64_t ld, int rows, int cols,
+               int rows_p, int cols_p, uint16_t *hi, uint16_t *lo, int64_t sstride,
+               int batch, hipStream_t s) {
+  const dim3 grid(static_cast<unsigned>((cols_p + 31) / 32),
+                  static_cast<unsigned>((rows_p + 31) / 32), static_cast<unsigned>(batch));
+  const int64_t dstride = static_cast<int64_t>(rows_p) * cols_p;
+  if (split && trans)
+    hipLaunchKernelGGL((pack_kernel<true, true>), grid, dim3(256), 0, s, src, ld, rows, cols,
+                       rows_p, cols_p, hi, lo, sstride, dstride);
+  else if (split)
+    hipLaunchKernelGGL((pack_kernel<true, false>), grid, dim3(256), 0, s, src, ld, rows, cols,
+                       rows_p, cols_p, hi, lo, sstride, dstride);
+  else if (trans)
+    hipLaunchKernelGGL((pack_kernel<false, true>), grid, dim3(256), 0, s, src, ld, rows, cols,
+                       rows_p, cols_p, hi, lo, sstride, dstride);
+  else
+    hipLaunchKernelGGL((pack_kernel<false, false>), grid, dim3(256), 0, s, src, ld, rows,
+                       cols, rows_p, cols_p, hi, lo, sstride, dstride);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+using C3 = Cfg<3, 128, 128, 2, 2>;
+using C3L = Cfg<3, 256, 128, 4, 2>;
+using C1 = Cfg<1, 128, 128, 2, 2>;
+using C1L = Cfg<1, 256, 128, 4, 2>;
+
+int env_variant() {
+  static const int v = [] {
+    const char *e = std::getenv("VELES_GEMM_BF16_VARIANT");
+    return e && *e ? std::atoi(e) : -1;
+  }();
+  return v;
+}
+
+vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha,
+                    const void *a, int64_t lda, int64_t sa, const void *b, int64_t ldb,
+                    int64_t sb, float beta, float *c, int64_t ldc, int64_t sc, int batch,
+                    int variant, hipStream_t s) {
+  VS_REQUIRE(m >= 0 && n >= 0 && k >= 0 && batch >= 0, "gemm_bf16: negative dimension");
+  if (m == 0 || n == 0 || batch == 0) return VS_OK;
+  VS_REQUIRE(a && b && c, "gemm_bf16: null pointer");
+  VS_REQUIRE(ldc >= n, "gemm_bf16: ldc < n");
+  VS_REQUIRE(lda >= (ta ? m : k) && ldb >= (tb ? k : n), "gemm_bf16: leading dimension too small");
+  if (batch > kMaxGridY) {
+    const size_t es = split ? sizeof(float) : sizeof(uint16_t);
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return gemm_impl(split, ta, tb, m, n, k, alpha,
+                       static_cast<const char *>(a) + b0 * sa * es, lda, sa,
+                       static_cast<const char *>(b) + b0 * sb * es, ldb, sb, beta,
+                       c + b0 * sc, ldc, sc, nb, variant, s);
+    });
+  }
+  if (variant < 0) variant = env_variant();
+  if (variant < 0) {
+    const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
+    variant = t256 >= 512 ? 1 : 0;
+  }
+  const int bm = variant == 1 ? 256 : 128, bn = 128;
+  const int mp = (m + bm - 1) / bm * bm, np = (n + bn - 1) / bn * bn;
+  const int kp = k == 0 ? kBK : (k + kBK - 1) / kBK * kBK;
+  const int ni = split ? 2 : 1;
+  const size_t ea = static_cast<size_t>(mp) * kp, eb = static_cast<size_t>(np) * kp;
+  DeviceBuffer buf;
+  VS_TRY(buf.alloc((ea + eb) * ni * batch * sizeof(uint16_t), s));
+  uint16_t *pa = buf.as<uint16_t>();
+  uint16_t *pb = pa + ea * ni * batch;
+  // A: logical (M x K), element (r, c) at a[r*lda + c] unless ta.
+  VS_TRY(pack(split, ta != 0, a, lda, m, k, mp, kp, pa, split ? pa + ea * batch : nullptr, sa,
+              batch, s));
+  // B: logical op(B)^T (N x K): element (n, k) at b[k*ldb + n] unless tb.
+  VS_TRY(pack(split, tb == 0, b, ldb, n, k, np, kp, pb, split ? pb + eb * batch : nullptr, sb,
+              batch, s));
+  Args g{};
+  g.a[0] = pa;
+  g.a[1] = split ? pa + ea * batch : nullptr;
+  g.b[0] = pb;
+  g.b[1] = split ? pb + eb * batch : nullptr;
+  g.sa = static_cast<int64_t>(ea);
+  g.sb = static_cast<int64_t>(eb);
+  g.kp = kp;
+  g.m = m;
+  g.n = n;
+  g.alpha = alpha;
+  g.beta = beta;
+  g.c = c;
+  g.ldc = ldc;
+  g.sc = sc;
+  if (split) return variant == 1 ? launch<C3L>(g, batch, s) : launch<C3>(g, batch, s);
+  return variant == 1 ? launch<C1L>(g, batch, s) : launch<C1>(g, batch, s);
+}
+
+}  // namespace
+}  // namespace gbf
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" {
+
+vs_status vs_gemm_bf16(int ta, int tb, int m, int n, int k, float alpha, const uint16_t *a,
+                       int64_t lda, const uint16_t *b, int64_t ldb, float beta, float *c,
+                       int64_t ldc, vs_stream_t stream) {
+  clear_error();
+  return gbf::gemm_impl(false, ta, tb, m, n, k, alpha, a, lda, 0, b, ldb, 0, beta, c, ldc, 0, 1,
+                        -1, static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_gemm_bf16_strided_batched(int ta, int tb, int m, int n, int k, float alpha,
+                                       const uint16_t *a, int64_t lda, int64_t sa,
+                                       const uint16_t *b, int64_t ldb, int64_t sb,
+                                       float beta, float *c, int64_t ldc, int64_t sc,
+                                       int batch, vs_stream_t stream) {
+  clear_error();
+  return gbf::gemm_impl(false, ta, tb, m, n, k, alpha, a, lda, sa, b, ldb, sb, beta, c, ldc, sc,
+                        batch, -1, static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_sgemm_bf16x3(int ta, int tb, int m, int n, int k, float alpha, const float *a,
+                          int64_t lda, const float *b, int64_t ldb, float beta, float *c,
+                          int64_t ldc, int variant, vs_stream_t stream) {
+  clear_error();
+  return gbf::gemm_impl(true, ta, tb, m, n, k, alpha, a, lda, 0, b, ldb, 0, beta, c, ldc, 0, 1,
+                        variant, static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_sgemm_bf16x3_strided_batched(int ta, int tb, int m, int n, int k, float alpha,
+                                          const float *a, int64_t lda, int64_t sa,
+                                          const float *b, int64_t ldb, int64_t sb, float beta,
+                                          float *c, int64_t ldc, int64_t sc, int batch,
+                                          vs_stream_t stream) {
+  clear_error();
+  return gbf::gemm_impl(true, ta, tb, m, n, k, alpha, a, lda, sa, b, ldb, sb, beta, c, ldc, sc,
+                        batch, -1, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -614,7 +614,11 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
   VS_REQUIRE(ldc >= n, "vs_sgemm: ldc (%lld) < n (%d)", (long long)ldc, n);
   VS_REQUIRE(lda >= (ta ? m : k) && ldb >= (tb ? k : n),
              "vs_sgemm: leading dimension too small");
-  VS_REQUIRE(batch <= 65535, "vs_sgemm: batch > 65535");
+  if (batch > kMaxGridY)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return sgemm_impl(variant, ta, tb, m, n, k, alpha, a + b0 * sa, lda, sa, b + b0 * sb,
+                        ldb, sb, beta, c + b0 * sc, ldc, sc, nb, s);
+    });
   GemmArgs g{m, n, k, alpha, beta, a, lda, sa, b, ldb, sb, c, ldc, sc};
   const auto al = [](const void *p) {
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0;

@@ -283,8 +283,13 @@ vs_status vs_dwt(int type, int order, int ext, const float *src, int len,
   VS_REQUIRE(src && hi && lo, "vs_dwt: null pointer");
   VS_REQUIRE(len > 0 && len % 2 == 0, "vs_dwt: length %d must be positive and even", len);
   VS_REQUIRE(ext >= 0 && ext <= 3, "vs_dwt: bad extension %d", ext);
-  VS_REQUIRE(batch >= 0 && batch <= 65535, "vs_dwt: batch out of range");
+  VS_REQUIRE(batch >= 0, "vs_dwt: negative batch");
   if (batch == 0) return VS_OK;
+  if (batch > kMaxGridY)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_dwt(type, order, ext, src + b0 * ss, len, ss, hi + b0 * os, lo + b0 * os, os,
+                    nb, stream);
+    });
   Taps t;
   VS_TRY(make_taps(type, order, &t));
   const dim3 grid(static_cast<unsigned>((len / 2 + kTile - 1) / kTile),
@@ -302,8 +307,13 @@ vs_status vs_swt(int type, int order, int level, int ext, const float *src,
   VS_REQUIRE(len > 0, "vs_swt: empty input");
   VS_REQUIRE(level >= 1 && level <= 24, "vs_swt: level %d out of range", level);
   VS_REQUIRE(ext >= 0 && ext <= 3, "vs_swt: bad extension %d", ext);
-  VS_REQUIRE(batch >= 0 && batch <= 65535, "vs_swt: batch out of range");
+  VS_REQUIRE(batch >= 0, "vs_swt: negative batch");
   if (batch == 0) return VS_OK;
+  if (batch > kMaxGridY)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_swt(type, order, level, ext, src + b0 * ss, len, ss, hi + b0 * os,
+                    lo + b0 * os, os, nb, stream);
+    });
   Taps t;
   VS_TRY(make_taps(type, order, &t));
   return launch_swt(t, level, ext, src, len, ss, hi, os, lo, os, batch,
@@ -335,7 +345,11 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
   }
   // Long signals: level by level through HBM (lo of level l feeds level
   // l+1, ping-ponging between two scratch bands; the last level writes lo).
-  VS_REQUIRE(batch <= 65535, "vs_swt_multilevel: batch out of range");
+  if (batch > kMaxGridY)
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_swt_multilevel(type, order, levels, ext, src + b0 * len, len,
+                               hi + b0 * levels * len, lo + b0 * len, nb, stream);
+    });
   DeviceBuffer tmp;
   const size_t band = static_cast<size_t>(len) * batch;
   VS_TRY(tmp.alloc(2 * band * sizeof(float), s));

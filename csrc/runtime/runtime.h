@@ -56,6 +56,19 @@ vs_status hip_status(hipError_t e, const char *what, const char *file,
       ::vs::fatal("%s failed: %s", #expr, ::vs::last_error());          \
   } while (0)
 
+// ----------------------------------------------------------- batching
+// Batched kernels put the batch on grid.y / grid.z (<= 65535 blocks); the
+// public entry points walk larger batches in chunks of this size.
+constexpr long long kMaxGridY = 65535;
+template <class F>
+vs_status batch_chunks(long long batch, F &&f) {
+  for (long long b0 = 0; b0 < batch; b0 += kMaxGridY) {
+    const long long nb = batch - b0 < kMaxGridY ? batch - b0 : kMaxGridY;
+    VS_TRY(f(b0, static_cast<int>(nb)));
+  }
+  return VS_OK;
+}
+
 // --------------------------------------------------------------- logging
 // VELES_LOG_LEVEL: 0 quiet (default), 1 dispatch decisions, 2 verbose.
 int log_level();

@@ -126,12 +126,44 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
                                    int64_t ldc, int64_t stride_c, int batch,
                                    vs_stream_t stream);
 
-/// Tuning entry point: one explicit SGEMM tile variant (0: 64x64x32,
-/// 1: 128x128x16, 2: 128x128x32, 3: 256x128x16, 4: 128x256x16).
+/// Tuning entry point: one explicit SGEMM tile variant (gen 1, k-major LDS:
+/// 0: 64x64x32, 1: 128x128x16, 2: 128x128x32, 3: 256x128x16, 4: 128x256x16;
+/// gen 2, k-contiguous LDS + interleaved schedule: 5: 128x128x32,
+/// 6: 256x128x32, 7: 128x256x32).
 vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
                            int k, float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,
                            int64_t ldc, vs_stream_t stream);
+
+/// bf16 matrix-core GEMM: C (fp32) = alpha op(A) op(B) + beta C with A, B
+/// bf16 (raw uint16 bit patterns), fp32 accumulation (v_mfma_f32_32x32x16_bf16).
+vs_status vs_gemm_bf16(int trans_a, int trans_b, int m, int n, int k,
+                       float alpha, const uint16_t *a, int64_t lda,
+                       const uint16_t *b, int64_t ldb, float beta, float *c,
+                       int64_t ldc, vs_stream_t stream);
+vs_status vs_gemm_bf16_strided_batched(int trans_a, int trans_b, int m, int n,
+                                       int k, float alpha, const uint16_t *a,
+                                       int64_t lda, int64_t stride_a,
+                                       const uint16_t *b, int64_t ldb,
+                                       int64_t stride_b, float beta, float *c,
+                                       int64_t ldc, int64_t stride_c,
+                                       int batch, vs_stream_t stream);
+/// Fast fp32 GEMM ("bf16x3"): fp32 operands split into bf16 hi + lo,
+/// C = hi hi + hi lo + lo hi on the bf16 matrix cores (~2^-16 relative
+/// error per product instead of 2^-24).  variant -1 = auto (0: 128x128,
+/// 1: 256x128 tiles).
+vs_status vs_sgemm_bf16x3(int trans_a, int trans_b, int m, int n, int k,
+                          float alpha, const float *a, int64_t lda,
+                          const float *b, int64_t ldb, float beta, float *c,
+                          int64_t ldc, int variant, vs_stream_t stream);
+vs_status vs_sgemm_bf16x3_strided_batched(int trans_a, int trans_b, int m,
+                                          int n, int k, float alpha,
+                                          const float *a, int64_t lda,
+                                          int64_t stride_a, const float *b,
+                                          int64_t ldb, int64_t stride_b,
+                                          float beta, float *c, int64_t ldc,
+                                          int64_t stride_c, int batch,
+                                          vs_stream_t stream);
 
 /* ------------------------------------------------------------------- FFT */
 /// Unnormalised complex FFT of `batch` contiguous interleaved signals of n

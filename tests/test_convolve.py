@@ -52,6 +52,17 @@ def test_handles_vs_brute(prefix, xlen, hlen, tol, corr):
     assert np.abs(res - verif).max() <= tol
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("xlen,hlen", [(4096, 64), (20000, 333)])
+def test_convolve_simd_gpu_direct_host_api(xlen, hlen):
+    """Above VELES_HOST_MAX_MACS the simd=1 host API stages to the GPU
+    direct kernel (smaller calls stay on the host reference by design)."""
+    x, h = _sin_x(xlen), _ramp_h(hlen)
+    np.testing.assert_allclose(capi.convolve_simd(1, x, h), _ref(x, h), atol=5e-3)
+    np.testing.assert_allclose(capi.convolve_simd(1, x, h, True), _ref(x, h, True),
+                               atol=5e-3)
+
+
 @pytest.mark.parametrize("simd", SIMDS)
 def test_convolve_simd_1024x50(simd):
     x, h = _sin_x(1024), _ramp_h(50)

@@ -129,3 +129,21 @@ def test_device_batched_and_multilevel(t, o, e):
         cur = nxt
         off += n
     np.testing.assert_allclose(pyr[:, off:], cur, atol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,o", [(D, 4), (S, 8), (C, 6), (D, 16)])
+@pytest.mark.parametrize("e", EXTS)
+def test_host_api_large_runs_on_gpu(t, o, e):
+    """Flag-less host API: length x taps >= VELES_GPU_MIN_ELEMS goes to the GPU
+    (staged through pinned bounce buffers); must equal the host reference."""
+    n = 1 << 18
+    x = (np.sin(np.arange(n) * 0.01) * 100).astype(np.float32)
+    hi, lo = capi.wavelet_apply(t, o, e, x)
+    vhi, vlo = capi.wavelet_apply(t, o, e, x, na=True)
+    np.testing.assert_allclose(hi, vhi, atol=5e-3)
+    np.testing.assert_allclose(lo, vlo, atol=5e-3)
+    shi, slo = capi.stationary_wavelet_apply(t, o, 2, e, x)
+    rhi, rlo = capi.stationary_wavelet_apply(t, o, 2, e, x, na=True)
+    np.testing.assert_allclose(shi, rhi, atol=5e-3)
+    np.testing.assert_allclose(slo, rlo, atol=5e-3)

@@ -58,6 +58,15 @@ _SIGNATURES = {
     "vs_sgemm_strided_batched": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _i64,
                                       _vp, _i64, _i64, _f, _vp, _i64, _i64, _i,
                                       _vp]),
+    "vs_gemm_bf16_strided_batched": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _i64, _vp,
+                                          _i64, _i64, _f, _vp, _i64, _i64, _i, _vp]),
+    "vs_sgemm_bf16x3": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _vp, _i64, _f, _vp,
+                             _i64, _i, _vp]),
+    "vs_sgemm_bf16x3_strided_batched": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _i64,
+                                             _vp, _i64, _i64, _f, _vp, _i64, _i64, _i,
+                                             _vp]),
+    "vs_sgemm_variant": (_i, [_i, _i, _i, _i, _i, _i, _f, _vp, _i64, _vp, _i64, _f,
+                              _vp, _i64, _vp]),
     "vs_fft_c2c": (_i, [_vp, _vp, _i, _i, _i, _vp]),
     "vs_fft_r2c": (_i, [_vp, _vp, _i, _i, _vp]),
     "vs_fft_c2r": (_i, [_vp, _vp, _i, _i, _vp]),

@@ -6,7 +6,7 @@ refuses to run if the native library is missing, instead of silently falling
 back), and runs the host reference semantics for CPU tensors.
 """
 from . import blas, elementwise, signal  # noqa: F401
-from .blas import matmul, matmul_transposed, sgemm  # noqa: F401
+from .blas import gemm_bf16, matmul, matmul_transposed, sgemm, sgemm_bf16x3  # noqa: F401
 from .elementwise import (add, affine, binary, complex_conjugate,  # noqa: F401
                           complex_multiply, convert, cos, exp, log, math,
                           minmax, mul, normalize2d, saxpy, sin, sub, sum_all)
@@ -15,7 +15,7 @@ from .signal import (conv1d, conv1d_algorithm, correlate, detect_peaks,  # noqa:
                      wavelet_filter)
 
 __all__ = [
-    "sgemm", "matmul", "matmul_transposed", "convert", "binary", "add", "sub",
+    "sgemm", "sgemm_bf16x3", "gemm_bf16", "matmul", "matmul_transposed", "convert", "binary", "add", "sub",
     "mul", "complex_multiply", "complex_conjugate", "affine", "saxpy", "math",
     "sin", "cos", "log", "exp", "sum_all", "minmax", "normalize2d", "conv1d",
     "correlate", "conv1d_algorithm", "fft", "rfft", "irfft", "dwt", "swt",
