@@ -164,3 +164,18 @@ def test_capi_large_array_goes_to_gpu():
     out = np.zeros(n, np.float32)
     capi.fn("int16_to_float")(capi.p(i16), n, capi.p(out))
     np.testing.assert_array_equal(out, i16.astype(np.float32))
+
+
+def test_mismatched_alignment_is_accepted():
+    """The reference EXPECT_DEATHs when src and dst have different 32-byte
+    alignment under AVX (arithmetic.cc:234-332): an AVX-only contract.  This
+    library has no alignment requirement (16-byte vector paths are chosen per
+    call), so the same calls must return the _na result instead of dying."""
+    src = np.arange(40, dtype=np.int16)
+    for s_off in (0, 1, 3):
+        for d_off in (0, 2):
+            s = src[s_off:s_off + 30]
+            out = np.zeros(30 + d_off, np.float32)[d_off:]
+            fn = getattr(capi._lib.lib(), "int16_to_float")
+            fn(capi.p(s), s.size, capi.p(out))
+            np.testing.assert_array_equal(out, s.astype(np.float32))

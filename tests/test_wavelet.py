@@ -147,3 +147,52 @@ def test_host_api_large_runs_on_gpu(t, o, e):
     rhi, rlo = capi.stationary_wavelet_apply(t, o, 2, e, x, na=True)
     np.testing.assert_allclose(shi, rhi, atol=5e-3)
     np.testing.assert_allclose(slo, rlo, atol=5e-3)
+
+
+def _wfn(name, res, args):
+    import ctypes
+    f = getattr(capi._lib.lib(), name)
+    f.restype = res
+    f.argtypes = args
+    return f
+
+
+def test_prepare_array_allocate_destination_recycle():
+    """Reference tests/wavelet.cc:44-86 in its non-AVX form (the GPU needs no
+    shifted copies: prepare = aligned copy), plus wavelet_recycle_source's
+    quarter-buffer carving (src/wavelet.c:138-165, non-AVX branch)."""
+    import ctypes
+    vp = ctypes.c_void_p
+    libc = ctypes.CDLL(None)
+    libc.free.argtypes = [vp]
+    prep = _wfn("wavelet_prepare_array", vp, [ctypes.c_int, vp, ctypes.c_size_t])
+    alloc = _wfn("wavelet_allocate_destination", vp, [ctypes.c_int, ctypes.c_size_t])
+    recycle = _wfn("wavelet_recycle_source", None,
+                   [ctypes.c_int, vp, ctypes.c_size_t] + [ctypes.POINTER(vp)] * 4)
+    x = np.arange(512, dtype=np.float32)
+    for order in (8, 4):
+        p = prep(order, x.ctypes.data, 512)
+        assert p % 64 == 0
+        got = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_float)), (512,))
+        np.testing.assert_array_equal(got, x)
+        libc.free(p)
+    d = alloc(8, 512)
+    assert d % 64 == 0
+    libc.free(d)
+    outs = [vp() for _ in range(4)]
+    recycle(8, x.ctypes.data, 512, *[ctypes.byref(o) for o in outs])
+    base = x.ctypes.data
+    assert [o.value for o in outs] == [base + 4 * 128 * i for i in range(4)]
+    recycle(8, x.ctypes.data, 510, *[ctypes.byref(o) for o in outs])
+    assert all(o.value is None for o in outs)
+
+
+def test_multilevel_chain_via_recycle():
+    """Two decimated levels chained the reference way: level-1 lo feeds
+    level 2, whose outputs land in the recycled quarters of the source."""
+    x = (np.sin(np.arange(256) * 0.3) * 10).astype(np.float32)
+    hi1, lo1 = capi.wavelet_apply(D, 8, 0, x)
+    hi2, lo2 = capi.wavelet_apply(D, 8, 0, lo1)
+    rhi2, rlo2 = capi.wavelet_apply(D, 8, 0, lo1, na=True)
+    np.testing.assert_allclose(hi2, rhi2, atol=5e-4)
+    np.testing.assert_allclose(lo2, rlo2, atol=5e-4)
