@@ -56,3 +56,20 @@ $(TEST_BIN): tests/native/capi_test.cpp $(LIB) $(HEADERS)
 
 clean:
 	rm -rf $(BUILD) $(LIB)
+
+# Host AddressSanitizer build of the library + native C API test (host code
+# only: device ASan / XNACK is not available on the GPU pool).  Runs the
+# host-reference paths on any machine: `make asan && ASAN_OPTIONS=detect_leaks=1 \
+#   build-asan/tests/capi_test --host`.
+ASAN_BUILD := build-asan
+ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer
+asan:
+	$(MAKE) BUILD=$(ASAN_BUILD) OPT="$(ASAN_FLAGS) -Xarch_host -fsanitize=address" \
+	    LIBDIR=$(ASAN_BUILD)/lib LIB=$(ASAN_BUILD)/lib/libvelessimd.so \
+	    TEST_BIN=$(ASAN_BUILD)/tests/capi_test lib
+	@mkdir -p $(ASAN_BUILD)/tests
+	$(HIPCC) $(ASAN_FLAGS) -Xarch_host -fsanitize=address -std=c++17 -Iinclude -Itests/native \
+	    tests/native/capi_test.cpp -o $(ASAN_BUILD)/tests/capi_test \
+	    -L$(ASAN_BUILD)/lib -lvelessimd -Wl,-rpath,'$$ORIGIN/../lib'
+
+.PHONY: asan

@@ -13,11 +13,15 @@
 #include <vector>
 
 #include <simd/arithmetic.h>
+#include <simd/convolve.h>
+#include <simd/correlate.h>
+#include <simd/detect_peaks.h>
 #include <simd/gpu.h>
 #include <simd/mathfun.h>
 #include <simd/matrix.h>
 #include <simd/memory.h>
 #include <simd/normalize.h>
+#include <simd/wavelet.h>
 
 #include "mini_test.h"
 
@@ -144,6 +148,90 @@ TEST_CASE(mathfun_vs_double) {
       CHECK_NEAR(e, y[i], 4.0 * std::nextafter(std::fabs(e), INFINITY) -
                               4.0 * std::fabs(e));
     }
+  }
+}
+
+// reference tests/convolve.cc:53-71 and tests/correlate.cc:53-71
+TEST_CASE(convolve_correlate_goldens) {
+  const float x[8] = {1, 2, 3, 4, 5, 6, 7, 8}, h[4] = {10, 9, 8, 7};
+  const float conv[11] = {10, 29, 56, 90, 124, 158, 192, 226, 170, 113, 56};
+  const float corr[11] = {7, 22, 46, 80, 114, 148, 182, 216, 187, 142, 80};
+  float y[11];
+  for (int simd = 0; simd < 2; simd++) {
+    convolve_simd(simd, x, 8, h, 4, y);
+    for (int i = 0; i < 11; i++) CHECK_NEAR(conv[i], y[i], 1e-4);
+    cross_correlate_simd(simd, x, 8, h, 4, y);
+    for (int i = 0; i < 11; i++) CHECK_NEAR(corr[i], y[i], 1e-4);
+  }
+  // every algorithm through the auto-selecting handle API
+  ConvolutionHandle hc = convolve_initialize(8, 4);
+  convolve(hc, x, h, y);
+  for (int i = 0; i < 11; i++) CHECK_NEAR(conv[i], y[i], 1e-3);
+  convolve_finalize(hc);
+}
+
+// reference tests/convolve.cc:73-137: FFT and overlap-save vs brute force
+TEST_CASE(convolve_fft_overlap_save_vs_brute) {
+  const int xl = 1021, hl = 50;
+  std::vector<float> x(xl), h(hl), ref(xl + hl - 1), y(xl + hl - 1);
+  for (int i = 0; i < xl; i++) x[i] = std::sin(static_cast<float>(i)) * 100;
+  for (int i = 0; i < hl; i++) h[i] = i / (hl - 1.f);
+  convolve_simd(0, x.data(), xl, h.data(), hl, ref.data());
+  ConvolutionFFTHandle f = convolve_fft_initialize(xl, hl);
+  convolve_fft(f, x.data(), h.data(), y.data());
+  convolve_fft_finalize(f);
+  for (int i = 0; i < xl + hl - 1; i++) CHECK_NEAR(ref[i], y[i], 1e-3);
+  ConvolutionOverlapSaveHandle o = convolve_overlap_save_initialize(xl, hl);
+  convolve_overlap_save(o, x.data(), h.data(), y.data());
+  convolve_overlap_save_finalize(o);
+  for (int i = 0; i < xl + hl - 1; i++) CHECK_NEAR(ref[i], y[i], 1e-3);
+  CrossCorrelationFFTHandle cf = cross_correlate_fft_initialize(xl, hl);
+  cross_correlate_fft(cf, x.data(), h.data(), y.data());
+  cross_correlate_fft_finalize(cf);
+  cross_correlate_simd(0, x.data(), xl, h.data(), hl, ref.data());
+  for (int i = 0; i < xl + hl - 1; i++) CHECK_NEAR(ref[i], y[i], 1e-3);
+}
+
+// reference tests/wavelet.cc:88-113 (db8, periodic, 0..31)
+TEST_CASE(wavelet_db8_golden) {
+  float src[32], hi[16], lo[16];
+  for (int i = 0; i < 32; i++) src[i] = i;
+  wavelet_apply_na(WAVELET_TYPE_DAUBECHIES, 8, EXTENSION_TYPE_PERIODIC, src, 32, hi, lo);
+  const float glo[16] = {1.4218407f, 4.2502678f, 7.0786950f, 9.9071221f, 12.735549f,
+                         15.563976f, 18.392403f, 21.220831f, 24.049258f, 26.877685f,
+                         29.706112f, 32.534539f, 35.362966f, 37.478254f, 45.304871f,
+                         28.840594f};
+  const float ghi_tail[3] = {-15.503000f, 5.5806650f, -1.3913732f};
+  for (int i = 0; i < 16; i++) CHECK_NEAR(glo[i], lo[i], 5e-4);
+  for (int i = 0; i < 13; i++) CHECK_NEAR(0.f, hi[i], 1e-4);
+  for (int i = 0; i < 3; i++) CHECK_NEAR(ghi_tail[i], hi[13 + i], 5e-4);
+  float *prep = wavelet_prepare_array(8, src, 32);
+  float *h2 = wavelet_allocate_destination(8, 32), *l2 = wavelet_allocate_destination(8, 32);
+  wavelet_apply(WAVELET_TYPE_DAUBECHIES, 8, EXTENSION_TYPE_PERIODIC, prep, 32, h2, l2);
+  for (int i = 0; i < 16; i++) {
+    CHECK_NEAR(hi[i], h2[i], 5e-4);
+    CHECK_NEAR(lo[i], l2[i], 5e-4);
+  }
+  free(prep);
+  free(h2);
+  free(l2);
+  CHECK_EQ(1, wavelet_validate_order(WAVELET_TYPE_DAUBECHIES, 8));
+  CHECK_EQ(0, wavelet_validate_order(WAVELET_TYPE_COIFLET, 8));
+}
+
+// reference tests/detect_peaks.cc:43-75
+TEST_CASE(detect_peaks_sin) {
+  const int n = 4000;
+  std::vector<float> x(n);
+  for (int i = 0; i < n; i++) x[i] = std::sin(i * 3.14159265f / 100);
+  for (int simd = 0; simd < 2; simd++) {
+    ExtremumPoint *pts = nullptr;
+    size_t count = 0;
+    detect_peaks(simd, x.data(), n, kExtremumTypeBoth, &pts, &count);
+    CHECK_EQ(40u, count);
+    for (size_t i = 0; i < count; i++)
+      CHECK_EQ(50 + 100 * static_cast<int>(i), pts[i].position);
+    free(pts);
   }
 }
 
