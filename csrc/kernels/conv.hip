@@ -275,7 +275,10 @@ int os_block_log(int hlen) {
 int select(int xlen, int hlen, int batch) {
   const long long ylen = static_cast<long long>(xlen) + hlen - 1;
   (void)batch;
-  if (hlen <= 32 || ylen <= 64) return VS_CONV_DIRECT;
+  // Direct only for very short filters or signals: at x = 2^20 the fused
+  // overlap-save kernel already beats the direct one from h = 16 on
+  // (405 vs 267 Gsamples/s, profiles/r1/conv_sweep_v2.log).
+  if (ylen <= 64 || hlen <= 8 || (hlen <= 32 && xlen < 4096)) return VS_CONV_DIRECT;
   const int los = os_block_log(hlen);
   const bool os_ok = (1 << los) - (hlen - 1) >= (1 << los) / 2;  // >= 50% useful
   int lm = 1;

@@ -145,7 +145,9 @@ __global__ __launch_bounds__(LdsGeom<LOGN>::kThreads) void c2c_lds_kernel(
 template <int LOG1>
 struct ColGeom {
   using PL = Plan<LOG1>;
-  static constexpr int COLS = PL::TPS >= 16 ? 16 : 256 / PL::TPS;
+  // <= 512 threads: at 1024 (LOG1 = 10, 16 columns) the 128-VGPR budget of
+  // 4 waves/SIMD spilled the 16-point-per-thread working set.
+  static constexpr int COLS = PL::TPS >= 64 ? 512 / PL::TPS : (PL::TPS >= 16 ? 16 : 256 / PL::TPS);
   static constexpr int kThreads = PL::TPS * COLS;
 };
 

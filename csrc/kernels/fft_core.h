@@ -129,12 +129,56 @@ __device__ __forceinline__ void dft16(float2 *v) {
   }
 }
 
+// cos / sin of pi k / 16, k = 0..15 (the 32-point twiddles)
+constexpr float kC32[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f,
+                            0.83146961230254523708f, 0.70710678118654752440f,
+                            0.55557023301960222474f, 0.38268343236508977173f,
+                            0.19509032201612826785f, 0.0f, -0.19509032201612826785f,
+                            -0.38268343236508977173f, -0.55557023301960222474f,
+                            -0.70710678118654752440f, -0.83146961230254523708f,
+                            -0.92387953251128675613f, -0.98078528040323044913f};
+constexpr float kS32[16] = {0.0f, 0.19509032201612826785f, 0.38268343236508977173f,
+                            0.55557023301960222474f, 0.70710678118654752440f,
+                            0.83146961230254523708f, 0.92387953251128675613f,
+                            0.98078528040323044913f, 1.0f, 0.98078528040323044913f,
+                            0.92387953251128675613f, 0.83146961230254523708f,
+                            0.70710678118654752440f, 0.55557023301960222474f,
+                            0.38268343236508977173f, 0.19509032201612826785f};
+
+// 32-point DFT: two 16-point DFTs (even / odd samples) and one twiddled
+// butterfly stage.
+template <bool INV>
+__device__ __forceinline__ void dft32(float2 *v) {
+  float2 e[16], o[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    e[j] = v[2 * j];
+    o[j] = v[2 * j + 1];
+  }
+  dft16<INV>(e);
+  dft16<INV>(o);
+  const float sg = INV ? 1.f : -1.f;
+#pragma unroll
+  for (int k = 1; k < 16; k++) {
+    if (k == 4) o[k] = w8_1<INV>(o[k]);
+    else if (k == 8) o[k] = rot90<INV>(o[k]);
+    else if (k == 12) o[k] = w8_3<INV>(o[k]);
+    else o[k] = cmul(o[k], make_float2(kC32[k], sg * kS32[k]));
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    v[k] = cadd(e[k], o[k]);
+    v[k + 16] = csub(e[k], o[k]);
+  }
+}
+
 template <int R, bool INV>
 __device__ __forceinline__ void dft(float2 *v) {
   if constexpr (R == 2) dft2<INV>(v);
   else if constexpr (R == 4) dft4<INV>(v);
   else if constexpr (R == 8) dft8<INV>(v);
-  else dft16<INV>(v);
+  else if constexpr (R == 16) dft16<INV>(v);
+  else dft32<INV>(v);
 }
 
 // LDS index with one pad slot per 16 complex elements.
@@ -151,10 +195,15 @@ struct Plan {
   static constexpr int E = LOGN >= 14 ? 32 : (LOGN >= 4 ? 16 : N);
   static constexpr int TPS = N / E;                // threads per signal
   static constexpr int SMALL = LOGN >= 4 ? LOGN % 4 : 0;
-  static constexpr int NPASS = LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1;
+  // N = 16384 runs 16 x 32 x 32 (3 passes, 2 LDS transposes) instead of
+  // 4 x 16 x 16 x 16: one butterfly of 32 per thread (E = 32) and a third
+  // fewer LDS round trips and barriers.
+  static constexpr bool R32 = LOGN == 14;
+  static constexpr int NPASS = R32 ? 3 : (LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1);
   static constexpr int kLds = N + N / 16 + 1;      // per-signal LDS (float2)
   // Radix of pass q (forward order: the odd radix first).
   static constexpr int radix(int q) {
+    if (R32) return q == 0 ? 16 : 32;
     return LOGN < 4 ? N : ((SMALL && q == 0) ? (1 << SMALL) : 16);
   }
   static constexpr int radix_rev(int q) { return radix(NPASS - 1 - q); }
@@ -184,12 +233,12 @@ struct Pass {
     for (int b = 0; b < NB; b++) {
       const int i = t + b * PL::TPS;
       if constexpr (P > 1) {
-        // w^j (j < R) as the product of the table entries w, w^2, w^4, w^8
-        // selected by the bits of j: 4 gathers instead of R - 1 and only 4
-        // live twiddles (at most 3 products, <= ~3 ulp).
+        // w^j (j < R) as the product of the table entries w, w^2, w^4, ...
+        // selected by the bits of j: log2 R gathers instead of R - 1 and
+        // only log2 R live twiddles (at most log2 R - 1 products).
         const int k = i & (P - 1);
         constexpr int S = PL::N / (P * R);
-        float2 wb[4];
+        float2 wb[R >= 32 ? 5 : 4];
 #pragma unroll
         for (int q = 0; (1 << q) < R; q++) wb[q] = tw[(1 << q) * k * S];
 #pragma unroll

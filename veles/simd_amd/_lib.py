@@ -74,6 +74,7 @@ _SIGNATURES = {
                        _vp]),
     "vs_conv1d_select": (_i, [_i, _i, _i]),
     "vs_conv1d_os_block": (_i, [_i]),
+    "vs_tune_set": (_i, [ctypes.c_char_p, _i]),
     "vs_dwt": (_i, [_i, _i, _i, _vp, _i, _i64, _vp, _vp, _i64, _i, _vp]),
     "vs_swt": (_i, [_i, _i, _i, _i, _vp, _i, _i64, _vp, _vp, _i64, _i, _vp]),
     "vs_swt_multilevel": (_i, [_i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp]),
