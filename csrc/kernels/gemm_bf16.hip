@@ -315,6 +315,181 @@ vs_status pack(bool split, bool trans, const void *src, int64_t ld, int rows, in
   return VS_OK;
 }
 
+// ------------------------------------------- LDS-DMA (glds) pipelined kernel
+// Large problems: operand tiles go global -> LDS with global_load_lds_dwordx4
+// (no VGPR round trip, 1 KiB per wave-instruction, LDS destination
+// wave-uniform base + 16 * lane), two LDS stages, the next k-tile's DMA
+// issued before the current tile's MFMAs and retired by one vmcnt(0) +
+// barrier per k-tile.  LDS images are [row][BK] bf16 with 16-byte chunk c
+// of row r stored at chunk c ^ ((r / S) & (NC - 1)) (S rows share a 256-byte
+// bank row): the XOR is applied to the per-lane SOURCE address of the DMA
+// and to the fragment read, so the 16-lane groups of ds_read_b128 hit 16
+// distinct bank groups (cdna_hip_programming.md §5.4 rule 21, T2).
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glob_void;
+
+template <int TERMS_, int BM_, int BN_, int BK_, int WM_, int WN_>
+struct GCfg {
+  static constexpr int TERMS = TERMS_, BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  static constexpr int NIMG = TERMS == 1 ? 1 : 2;
+  static constexpr int kThreads = 64 * WM * WN, kWaves = WM * WN;
+  static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static constexpr int NC = BK / 8;        // 16-byte chunks per row
+  static constexpr int RB = BK * 2;        // row bytes
+  static constexpr int S = 256 / RB;       // rows per 256-byte bank row
+  static constexpr int RPI = 1024 / RB;    // rows per glds wave-instruction
+  static constexpr int kImgA = BM * RB, kImgB = BN * RB;  // bytes
+  static constexpr int kStage = NIMG * (kImgA + kImgB);
+  static constexpr int kLdsBytes = 2 * kStage;
+  static constexpr int kInstrA = kImgA / 1024 / kWaves;   // per wave, per image
+  static constexpr int kInstrB = kImgB / 1024 / kWaves;
+  static_assert(kInstrA * 1024 * kWaves == kImgA && kInstrB * 1024 * kWaves == kImgB,
+                "image not divisible into whole glds instructions per wave");
+  static_assert(BK % 16 == 0 && RB <= 1024, "BK");
+};
+
+template <class C>
+__device__ __forceinline__ int swz(int row, int c) {
+  return c ^ ((row / C::S) & (C::NC - 1));
+}
+
+// DMA one image tile (ROWS x BK at row0, k0) into the LDS image at `dst`.
+template <class C, int INSTR>
+__device__ __forceinline__ void dma_image(const uint16_t *__restrict__ img, int64_t kp,
+                                          int row0, int k0, uint8_t *dst, int wave,
+                                          int lane) {
+#pragma unroll
+  for (int i = 0; i < INSTR; i++) {
+    const int j = wave * INSTR + i;            // instruction index in the image
+    const int row = j * C::RPI + lane / C::NC;  // tile row this lane fills
+    const int pc = lane % C::NC;                // physical chunk it fills
+    const int c = swz<C>(row, pc);              // logical chunk stored there
+    const uint16_t *src = img + static_cast<int64_t>(row0 + row) * kp + k0 + 8 * c;
+    __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(dst + j * 1024), 16, 0,
+                                     0);
+  }
+}
+
+template <class C>
+__device__ __forceinline__ bf16x8 gfrag(const uint8_t *img, int row, int c) {
+  return *reinterpret_cast<const bf16x8 *>(img + row * C::RB + swz<C>(row, c) * 16);
+}
+
+template <class C>
+__global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
+  extern __shared__ __attribute__((aligned(1024))) uint8_t glds_lds[];
+  constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
+  const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
+  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
+  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  unsigned tm, tn;
+  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
+  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
+  const int64_t kp = g.kp;
+  const uint16_t *A[2], *B[2];
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    A[i] = g.a[i] + blockIdx.z * g.sa;
+    B[i] = g.b[i] + blockIdx.z * g.sb;
+  }
+  float *Cp = g.c + blockIdx.z * g.sc;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int arow = wm * (C::BM / C::WM) + lrow;
+  const int brow = wn * (C::BN / C::WN) + lrow;
+
+  auto img_a = [&](int buf, int i) { return glds_lds + buf * C::kStage + i * C::kImgA; };
+  auto img_b = [&](int buf, int i) {
+    return glds_lds + buf * C::kStage + NI * C::kImgA + i * C::kImgB;
+  };
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+      dma_image<C, C::kInstrA>(A[i], kp, m0, k0, img_a(buf, i), wid, lane);
+      dma_image<C, C::kInstrB>(B[i], kp, n0, k0, img_b(buf, i), wid, lane);
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+
+  const int nk = g.kp / C::BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt++) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
+#pragma unroll
+    for (int ks = 0; ks < C::BK / 16; ks++) {
+      const int c = 2 * ks + lh;
+      bf16x8 fa[NI][TM], fb[NI][TN];
+#pragma unroll
+      for (int i = 0; i < NI; i++) {
+#pragma unroll
+        for (int x = 0; x < TM; x++) fa[i][x] = gfrag<C>(img_a(cur, i), arow + 32 * x, c);
+#pragma unroll
+        for (int y = 0; y < TN; y++) fb[i][y] = gfrag<C>(img_b(cur, i), brow + 32 * y, c);
+      }
+#pragma unroll
+      for (int x = 0; x < TM; x++)
+#pragma unroll
+        for (int y = 0; y < TN; y++) {
+          if (C::TERMS == 3) {
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][x], fb[0][y],
+                                                                acc[x][y], 0, 0, 0);
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[1][y],
+                                                                acc[x][y], 0, 0, 0);
+          }
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[0][y],
+                                                              acc[x][y], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const bool use_beta = g.beta != 0.f;
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      const int col = n0 + brow + 32 * y;
+      if (col >= g.n) continue;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int row = m0 + arow - lrow + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < g.m) {
+          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+          float v = g.alpha * acc[x][y][r];
+          if (use_beta) v += g.beta * *pc;
+          *pc = v;
+        }
+      }
+    }
+}
+
+template <class C>
+vs_status launch_glds(const Args &g, int batch, hipStream_t s) {
+  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_glds_kernel<C>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes));
+  const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
+                                               ((g.n + C::BN - 1) / C::BN));
+  hipLaunchKernelGGL(gemm_glds_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
+                     dim3(C::kThreads), C::kLdsBytes, s, g);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+using G1 = GCfg<1, 256, 256, 64, 2, 4>;   // bf16: 128 KiB LDS, 8 waves of 128 x 64
+using G3 = GCfg<3, 256, 128, 32, 4, 2>;   // bf16x3: 96 KiB LDS, 8 waves of 64 x 64
+
 using C3 = Cfg<3, 128, 128, 2, 2>;
 using C3L = Cfg<3, 256, 128, 4, 2>;
 using C1 = Cfg<1, 128, 128, 2, 2>;
@@ -349,11 +524,17 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   if (variant < 0) variant = env_variant();
   if (variant < 0) {
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
-    variant = t256 >= 512 ? 1 : 0;
+    variant = t256 >= 256 ? 2 : (t256 >= 128 ? 1 : 0);
   }
-  const int bm = variant == 1 ? 256 : 128, bn = 128;
+  VS_REQUIRE(variant >= 0 && variant <= 2, "gemm_bf16: unknown variant %d", variant);
+  int bm = variant == 1 ? 256 : 128, bn = 128, bk = kBK;
+  if (variant == 2) {
+    bm = split ? G3::BM : G1::BM;
+    bn = split ? G3::BN : G1::BN;
+    bk = split ? G3::BK : G1::BK;
+  }
   const int mp = (m + bm - 1) / bm * bm, np = (n + bn - 1) / bn * bn;
-  const int kp = k == 0 ? kBK : (k + kBK - 1) / kBK * kBK;
+  const int kp = k == 0 ? bk : (k + bk - 1) / bk * bk;
   const int ni = split ? 2 : 1;
   const size_t ea = static_cast<size_t>(mp) * kp, eb = static_cast<size_t>(np) * kp;
   DeviceBuffer buf;
@@ -381,6 +562,7 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   g.c = c;
   g.ldc = ldc;
   g.sc = sc;
+  if (variant == 2) return split ? launch_glds<G3>(g, batch, s) : launch_glds<G1>(g, batch, s);
   if (split) return variant == 1 ? launch<C3L>(g, batch, s) : launch<C3>(g, batch, s);
   return variant == 1 ? launch<C1L>(g, batch, s) : launch<C1>(g, batch, s);
 }

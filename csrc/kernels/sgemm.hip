@@ -266,7 +266,9 @@ struct TileIO2 {
   static constexpr int kLoads = BMN * BK / 4 / THREADS;
   static_assert(kLoads * 4 * THREADS == BMN * BK, "tile not divisible");
   static constexpr int P = KC ? BK + 4 : BMN + 4;      // LDS pitch (floats)
-  static constexpr int kFragReads = KC ? 1 : 4;        // ds_read per frag()
+  // ds_read instructions per frag(): the four scalar reads of an MN-contiguous
+  // image are merged by the compiler into two ds_read2_b32
+  static constexpr int kFragReads = KC ? 1 : 2;
   static constexpr int kFloats = KC ? BMN * P : BK * P;
 
   // Thread's (mn, k) coordinates of float4 number l of the tile.

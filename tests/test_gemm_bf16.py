@@ -90,3 +90,21 @@ def test_fake_tensor_shapes():
         b = torch.empty(16, 32)
         assert ops.sgemm_bf16x3(a, b).shape == (4, 8, 32)
         assert ops.gemm_bf16(a.bfloat16(), b.bfloat16(), False, False).dtype == torch.float32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, True)])
+def test_large_shapes_use_lds_dma_kernel(ta, tb):
+    """>= 256 tiles of 256 x 128 select the global_load_lds pipelined kernel
+    (ragged M / N / K exercise the zero-padded images)."""
+    m, n, k = 4000, 2100, 520
+    g = torch.Generator(device="cuda").manual_seed(3)
+    a = torch.rand((k, m) if ta else (m, k), device="cuda", generator=g) * 2 - 1
+    b = torch.rand((n, k) if tb else (k, n), device="cuda", generator=g) * 2 - 1
+    ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
+    c3 = ops.sgemm_bf16x3(a, b, ta, tb)
+    assert (c3.double() - ref).abs().max().item() <= 8 * 2.0 ** -17 * math.sqrt(k) + 1e-6
+    ah, bh = a.bfloat16(), b.bfloat16()
+    c1 = ops.gemm_bf16(ah, bh, ta, tb)
+    ref1 = (ah.double().T if ta else ah.double()) @ (bh.double().T if tb else bh.double())
+    assert (c1.double() - ref1).abs().max().item() <= 2e-6 * k + 1e-6

@@ -36,6 +36,8 @@ def main():
                                                      b.data_ptr(), n, 0.0, c.data_ptr(), n, 0, s),
             "bf16x3_v1": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
                                                      b.data_ptr(), n, 0.0, c.data_ptr(), n, 1, s),
+            "bf16x3_v2": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
+                                                     b.data_ptr(), n, 0.0, c.data_ptr(), n, 2, s),
             "bf16": lambda: lib.vs_gemm_bf16_strided_batched(0, 0, n, n, n, 1.0, ah.data_ptr(),
                                                              n, 0, bh.data_ptr(), n, 0, 0.0,
                                                              c.data_ptr(), n, 0, 1, s),
