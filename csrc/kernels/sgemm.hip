@@ -887,9 +887,13 @@ bool launch_cfg3x16(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipS
 // 16-k group per tile; A chunk swizzle for 4-chunk rows read by 16x16
 // fragments: c ^ 3 * ((row >> 3) & 1) (the 16-lane groups of ds_read_b128
 // then hit 16 distinct bank groups).
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, bool ASM_ = true>
 struct Cfg4 {
   static constexpr int BM = BM_, BN = BN_, BK = 16, WM = WM_, WN = WN_;
+  // fragment reads as inline asm (invisible to the wait-insertion pass); the
+  // 1024-thread configuration keeps compiler-visible reads: with asm reads it
+  // exceeded its 128-VGPR budget
+  static constexpr bool ASM = ASM_;
   static constexpr int kThreads = 64 * WM * WN, kWaves = WM * WN;
   static constexpr int RBA = BK * 4, RBB = BN * 4;
   static constexpr int kImgA = BM * RBA, kImgB = BK * RBB;
@@ -948,15 +952,41 @@ struct Gen4 {
     }
   }
 
+  // Fragment reads are inline asm: the compiler's wait insertion cannot see
+  // them, so it adds no vmcnt(0) for the DMA still in flight into the other
+  // stages (with builtin reads it drained the fresh DMA before every second
+  // tile).  Ordering is explicit instead: the tile's DMA was retired by the
+  // counted vmcnt + barrier before this point, the reads are waited for with
+  // lgkmcnt(0), and sched_barrier(0) keeps the MFMAs behind that wait
+  // (cdna_hip_programming.md §5.4 rule 18).
   __device__ static void compute(const uint8_t *ia, floatx4 (&acc)[TM][TN], int arow,
                                  int bcol, int q) {
-    const float *ib = reinterpret_cast<const float *>(ia + C::kImgA);
     float4 fa[TM];
     float fb[TN][4];
+    if constexpr (!C::ASM) {
+      const float *ib = reinterpret_cast<const float *>(ia + C::kImgA);
+#pragma unroll
+      for (int x = 0; x < TM; x++) {
+        const int r = arow + 16 * x;
+        fa[x] = *reinterpret_cast<const float4 *>(ia + r * C::RBA + aswz4(r, q) * 16);
+      }
+#pragma unroll
+      for (int sidx = 0; sidx < 4; sidx++) {
+        const int kr = 4 * q + sidx;
+#pragma unroll
+        for (int y = 0; y < TN; y++) {
+          const int col = bcol + 16 * y;
+          fb[y][sidx] = ib[kr * C::BN + 4 * ((col >> 2) ^ (((kr >> 2) & 1) << 2)) + (col & 3)];
+        }
+      }
+    } else {
+    const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ia));
+    const uint32_t lb = la + C::kImgA;
 #pragma unroll
     for (int x = 0; x < TM; x++) {
       const int r = arow + 16 * x;
-      fa[x] = *reinterpret_cast<const float4 *>(ia + r * C::RBA + aswz4(r, q) * 16);
+      const uint32_t addr = la + r * C::RBA + aswz4(r, q) * 16;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(fa[x]) : "v"(addr) : "memory");
     }
 #pragma unroll
     for (int sidx = 0; sidx < 4; sidx++) {
@@ -964,8 +994,13 @@ struct Gen4 {
 #pragma unroll
       for (int y = 0; y < TN; y++) {
         const int col = bcol + 16 * y;
-        fb[y][sidx] = ib[kr * C::BN + 4 * ((col >> 2) ^ (((kr >> 2) & 1) << 2)) + (col & 3)];
+        const uint32_t addr =
+            lb + 4 * (kr * C::BN + 4 * ((col >> 2) ^ (((kr >> 2) & 1) << 2)) + (col & 3));
+        asm volatile("ds_read_b32 %0, %1" : "=v"(fb[y][sidx]) : "v"(addr) : "memory");
       }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int sidx = 0; sidx < 4; sidx++)
@@ -1053,9 +1088,9 @@ bool launch_cfg4(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipStre
   return true;
 }
 
-using Cfg4A = Cfg4<128, 128, 2, 2>;   // 48 KiB LDS (3 stages), 4 waves of 64 x 64
+using Cfg4A = Cfg4<128, 128, 2, 2, false>;  // 48 KiB LDS (3 stages), 4 waves of 64 x 64
 using Cfg4B = Cfg4<256, 128, 4, 2>;   // 72 KiB LDS, 8 waves of 64 x 64
-using Cfg4C = Cfg4<256, 256, 4, 4>;   // 96 KiB LDS, 16 waves of 64 x 64
+using Cfg4C = Cfg4<256, 256, 4, 4, false>;  // 96 KiB LDS, 16 waves of 64 x 64
 
 using Cfg3A = Cfg3<256, 128, 32, 4, 2>;   // 96 KiB LDS, 8 waves of 64 x 64
 using Cfg3B = Cfg3<128, 128, 32, 2, 2>;   // 64 KiB LDS, 2 blocks / CU
@@ -1099,12 +1134,16 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
   if (variant < 0) variant = default_variant();
   if (variant < 0) {
     // Largest tile that still gives every CU work (A/B on MI355X,
-    // profiles/r1/sgemm_variants.md): 256x128 (gen 1, BK 16) when >= 512
-    // tiles, 128x128 (gen 2, BK 32, interleaved schedule) when >= 256, else
-    // 64x64.
+    // profiles/r1/sgemm_variants.md): the three-stage LDS-DMA kernels when
+    // the shape is NN and whole tiles (256x256 from 256 tiles, else 128x128),
+    // otherwise 256x128 (gen 1) / 128x128 (gen 2) / 64x64 register-staged.
     const long t128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
-    variant = t256 >= 512 ? 3 : (t128 >= 256 ? 5 : 0);
+    const long t256sq = static_cast<long>((m + 255) / 256) * ((n + 255) / 256) * batch;
+    if (t256sq >= 256) variant = 15;       // falls back to 3 unless NN whole tiles
+    else if (t128 >= 256) variant = 13;    // falls back to 5
+    else if (t256 >= 512) variant = 3;
+    else variant = 0;
   }
   switch (variant) {
     case 0: launch_cfg<CfgSmall>(g, ta, tb, vec, batch, s); break;
@@ -1139,6 +1178,7 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
     case 15:
       if (!launch_cfg4<Cfg4C>(g, ta, tb, vec, batch, s)) launch_cfg<CfgC>(g, ta, tb, vec, batch, s);
       break;
+
     default:
       set_error("vs_sgemm: unknown variant %d", variant);
       return VS_ERR_INVALID;
@@ -1169,7 +1209,7 @@ vs_status vs_sgemm_strided_batched(int ta, int tb, int m, int n, int k,
                         beta, c, ldc, sc, batch, static_cast<hipStream_t>(stream));
 }
 
-// Tuning entry point: run one explicit tile variant (0..7).
+// Tuning entry point: run one explicit tile variant (0..15, include/simd/gpu.h).
 vs_status vs_sgemm_variant(int variant, int ta, int tb, int m, int n, int k,
                            float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,

@@ -129,7 +129,10 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
 /// Tuning entry point: one explicit SGEMM tile variant (gen 1, k-major LDS:
 /// 0: 64x64x32, 1: 128x128x16, 2: 128x128x32, 3: 256x128x16, 4: 128x256x16;
 /// gen 2, k-contiguous LDS + interleaved schedule: 5: 128x128x32,
-/// 6: 256x128x32, 7: 128x256x32).
+/// 6: 256x128x32, 7: 128x256x32; NN whole-tile LDS-DMA kernels (other shapes
+/// fall back to gen 1/2): gen 3 8: 256x128x32, 9: 128x128x32, 10: 256x256x16,
+/// 11/12: the 16x16x4-MFMA forms of 8/9; gen 4, three-stage DMA ring:
+/// 13: 128x128, 14: 256x128, 15: 256x256 (BK 16)).
 vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
                            int k, float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,
