@@ -118,6 +118,19 @@ def main():
     secondary = {"torch_matmul_fp32_gflops": round(torch_gflops, 1),
                  "sgemm_max_abs_err": err}
 
+    # Fast-fp32 mode on the bf16 matrix cores (hi/lo split, 3 products;
+    # ~2^-17 relative per product): reported for context, NOT the headline.
+    if hasattr(lib, "vs_sgemm_bf16x3"):
+        def x3_step():
+            st = lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, pa, n, pb, n, 0.0, pc, n, -1, stream)
+            if st:
+                raise RuntimeError(lib.vs_last_error().decode())
+        dt3 = _timed(x3_step, max(5, args.steps // 2), 3, dist_on)
+        err3 = (c[:256].double() - ref).abs().max().item()
+        secondary["sgemm_bf16x3_gflops"] = round(
+            2.0 * n ** 3 * max(5, args.steps // 2) * world / dt3 / 1e9, 1)
+        secondary["sgemm_bf16x3_max_abs_err"] = err3
+
     # ----------------------------------------------------------------- conv
     if not args.no_conv and hasattr(lib, "vs_conv1d"):
         x = torch.randn((CONV_BATCH, CONV_LEN), device="cuda", generator=g)
