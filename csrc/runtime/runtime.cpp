@@ -7,6 +7,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <vector>
 
 namespace vs {
@@ -149,6 +150,20 @@ class ScratchPool {
     const size_t sz = round(bytes);
     int dev = 0;
     (void)hipGetDevice(&dev);
+    if (capturing(stream)) {
+      // Inside a HIP-graph capture: a stream-ordered allocation becomes a
+      // graph memory node owned by the graph (freed by the matching
+      // hipFreeAsync node); the cache (event queries, host-side reuse) is
+      // not usable while capturing.
+      void *p = nullptr;
+      if (hipMallocAsync(&p, sz, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      std::lock_guard<std::mutex> lock(mu_);
+      graph_.insert(p);
+      return p;
+    }
     {
       std::lock_guard<std::mutex> lock(mu_);
       for (auto it = free_.lower_bound(sz); it != free_.end(); ++it) {
@@ -180,6 +195,10 @@ class ScratchPool {
 
   void release(void *p, hipStream_t stream) {
     std::lock_guard<std::mutex> lock(mu_);
+    if (graph_.erase(p)) {
+      (void)hipFreeAsync(p, stream);
+      return;
+    }
     auto it = live_.find(p);
     if (it == live_.end()) return;
     Block b = it->second;
@@ -216,9 +235,18 @@ class ScratchPool {
     const size_t g = 2u << 20;
     return (b + g - 1) / g * g;
   }
+  static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (s == nullptr || hipStreamIsCapturing(s, &st) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return st == hipStreamCaptureStatusActive;
+  }
   std::mutex mu_;
   std::multimap<size_t, Block> free_;
   std::map<void *, Block> live_;
+  std::set<void *> graph_;  // captured (graph-owned) allocations
 };
 
 vs_status DeviceBuffer::alloc(size_t bytes, hipStream_t stream) {

@@ -2,3 +2,4 @@
 from .config import Config, config  # noqa: F401
 from .profiling import range_pop, range_push, trace_range  # noqa: F401
 from .timing import GpuTimer, benchmark  # noqa: F401
+from .graphs import CapturedCall  # noqa: F401
