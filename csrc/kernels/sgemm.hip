@@ -887,9 +887,11 @@ bool launch_cfg3x16(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipS
 // 16-k group per tile; A chunk swizzle for 4-chunk rows read by 16x16
 // fragments: c ^ 3 * ((row >> 3) & 1) (the 16-lane groups of ds_read_b128
 // then hit 16 distinct bank groups).
-template <int BM_, int BN_, int WM_, int WN_, bool ASM_ = true>
+template <int BM_, int BN_, int WM_, int WN_, bool ASM_ = true, int BK_ = 16>
 struct Cfg4 {
-  static constexpr int BM = BM_, BN = BN_, BK = 16, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
+  static constexpr int NC = BK / 4;  // 16-byte chunks per A row (4 or 8)
+  static_assert(BK == 16 || BK == 32, "BK");
   // fragment reads as inline asm (invisible to the wait-insertion pass); the
   // 1024-thread configuration keeps compiler-visible reads: with asm reads it
   // exceeded its 128-VGPR budget
@@ -903,10 +905,19 @@ struct Cfg4 {
   static constexpr int kInstr = kInstrA + kInstrB;  // DMA instructions per wave per tile
   static_assert(kInstrA * 1024 * kWaves == kImgA && kInstrB * 1024 * kWaves == kImgB,
                 "tile not divisible into whole DMA instructions per wave");
-  static_assert(kInstr >= 1 && kInstr <= 8, "vmcnt immediates below");
+  static_assert(kInstr >= 1 && kInstr <= 16, "vmcnt immediates below");
 };
 
-__device__ __forceinline__ int aswz4(int row, int c) { return c ^ (3 * ((row >> 3) & 1)); }
+// A-image chunk swizzle for 16x16 fragment reads (lanes 0-15 of a quarter
+// read rows 0-15 at chunk 4g + q): conflict-free ds_read_b128 groups.
+//   4-chunk rows (BK 16):  c ^ 3 ((row >> 3) & 1)
+//   8-chunk rows (BK 32):  c ^ ((row >> 1) & 7)
+template <int NC>
+__device__ __forceinline__ int aswz(int row, int c) {
+  if constexpr (NC == 4) return c ^ (3 * ((row >> 3) & 1));
+  else return c ^ ((row >> 1) & 7);
+}
+__device__ __forceinline__ int aswz4(int row, int c) { return aswz<4>(row, c); }
 
 // s_waitcnt vmcnt(N) through the builtin, not inline asm: the compiler's
 // wait-insertion pass understands the builtin (an asm wait is opaque to it,
@@ -934,8 +945,8 @@ struct Gen4 {
 #pragma unroll
     for (int i = 0; i < C::kInstrA; i++) {
       const int j = wid * C::kInstrA + i;
-      const int row = j * (1024 / C::RBA) + lane / 4;
-      const int c = aswz4(row, lane % 4);
+      const int row = j * (1024 / C::RBA) + lane / C::NC;
+      const int c = aswz<C::NC>(row, lane % C::NC);
       const float *src = A + static_cast<int64_t>(m0 + row) * g.lda + k0 + 4 * c;
       __builtin_amdgcn_global_load_lds((glob_void_t *)src, (lds_void_t *)(ia + j * 1024), 16,
                                        0, 0);
@@ -961,6 +972,12 @@ struct Gen4 {
   // (cdna_hip_programming.md §5.4 rule 18).
   __device__ static void compute(const uint8_t *ia, floatx4 (&acc)[TM][TN], int arow,
                                  int bcol, int q) {
+#pragma unroll
+    for (int gk = 0; gk < C::BK / 16; gk++) group(ia, acc, arow, bcol, q, gk);
+  }
+
+  __device__ static void group(const uint8_t *ia, floatx4 (&acc)[TM][TN], int arow,
+                               int bcol, int q, int gk) {
     float4 fa[TM];
     float fb[TN][4];
     if constexpr (!C::ASM) {
@@ -968,11 +985,12 @@ struct Gen4 {
 #pragma unroll
       for (int x = 0; x < TM; x++) {
         const int r = arow + 16 * x;
-        fa[x] = *reinterpret_cast<const float4 *>(ia + r * C::RBA + aswz4(r, q) * 16);
+        fa[x] = *reinterpret_cast<const float4 *>(ia + r * C::RBA +
+                                                  aswz<C::NC>(r, 4 * gk + q) * 16);
       }
 #pragma unroll
       for (int sidx = 0; sidx < 4; sidx++) {
-        const int kr = 4 * q + sidx;
+        const int kr = 16 * gk + 4 * q + sidx;
 #pragma unroll
         for (int y = 0; y < TN; y++) {
           const int col = bcol + 16 * y;
@@ -980,27 +998,33 @@ struct Gen4 {
         }
       }
     } else {
-    const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ia));
-    const uint32_t lb = la + C::kImgA;
+      // Fragment reads are inline asm: the compiler's wait insertion cannot
+      // see them, so it adds no vmcnt(0) for the DMA still in flight into
+      // the other stages.  Ordering is explicit instead: the tile's DMA was
+      // retired by the counted vmcnt + barrier before this point, the reads
+      // are waited for with lgkmcnt(0), and sched_barrier(0) keeps the MFMAs
+      // behind that wait (cdna_hip_programming.md §5.4 rule 18).
+      const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ia));
+      const uint32_t lb = la + C::kImgA;
 #pragma unroll
-    for (int x = 0; x < TM; x++) {
-      const int r = arow + 16 * x;
-      const uint32_t addr = la + r * C::RBA + aswz4(r, q) * 16;
-      asm volatile("ds_read_b128 %0, %1" : "=v"(fa[x]) : "v"(addr) : "memory");
-    }
-#pragma unroll
-    for (int sidx = 0; sidx < 4; sidx++) {
-      const int kr = 4 * q + sidx;
-#pragma unroll
-      for (int y = 0; y < TN; y++) {
-        const int col = bcol + 16 * y;
-        const uint32_t addr =
-            lb + 4 * (kr * C::BN + 4 * ((col >> 2) ^ (((kr >> 2) & 1) << 2)) + (col & 3));
-        asm volatile("ds_read_b32 %0, %1" : "=v"(fb[y][sidx]) : "v"(addr) : "memory");
+      for (int x = 0; x < TM; x++) {
+        const int r = arow + 16 * x;
+        const uint32_t addr = la + r * C::RBA + aswz<C::NC>(r, 4 * gk + q) * 16;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fa[x]) : "v"(addr) : "memory");
       }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sidx = 0; sidx < 4; sidx++) {
+        const int kr = 16 * gk + 4 * q + sidx;
+#pragma unroll
+        for (int y = 0; y < TN; y++) {
+          const int col = bcol + 16 * y;
+          const uint32_t addr =
+              lb + 4 * (kr * C::BN + 4 * ((col >> 2) ^ (((kr >> 2) & 1) << 2)) + (col & 3));
+          asm volatile("ds_read_b32 %0, %1" : "=v"(fb[y][sidx]) : "v"(addr) : "memory");
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int sidx = 0; sidx < 4; sidx++)
@@ -1091,6 +1115,9 @@ bool launch_cfg4(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipStre
 using Cfg4A = Cfg4<128, 128, 2, 2, false>;  // 48 KiB LDS (3 stages), 4 waves of 64 x 64
 using Cfg4B = Cfg4<256, 128, 4, 2>;   // 72 KiB LDS, 8 waves of 64 x 64
 using Cfg4C = Cfg4<256, 256, 4, 4, false>;  // 96 KiB LDS, 16 waves of 64 x 64
+using Cfg4E = Cfg4<128, 128, 2, 2, true, 32>;   // 96 KiB LDS: 1 block / CU, 1 wave / SIMD
+using Cfg4F = Cfg4<128, 128, 2, 2, false, 32>;
+using Cfg4G = Cfg4<256, 128, 4, 2, true, 32>;   // 144 KiB LDS
 
 using Cfg3A = Cfg3<256, 128, 32, 4, 2>;   // 96 KiB LDS, 8 waves of 64 x 64
 using Cfg3B = Cfg3<128, 128, 32, 2, 2>;   // 64 KiB LDS, 2 blocks / CU
@@ -1177,6 +1204,15 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
       break;
     case 15:
       if (!launch_cfg4<Cfg4C>(g, ta, tb, vec, batch, s)) launch_cfg<CfgC>(g, ta, tb, vec, batch, s);
+      break;
+    case 16:
+      if (!launch_cfg4<Cfg4E>(g, ta, tb, vec, batch, s)) launch_cfg2<Cfg2A>(g, ta, tb, vec, batch, s);
+      break;
+    case 17:
+      if (!launch_cfg4<Cfg4F>(g, ta, tb, vec, batch, s)) launch_cfg2<Cfg2A>(g, ta, tb, vec, batch, s);
+      break;
+    case 18:
+      if (!launch_cfg4<Cfg4G>(g, ta, tb, vec, batch, s)) launch_cfg<CfgC>(g, ta, tb, vec, batch, s);
       break;
 
     default:
