@@ -1168,7 +1168,7 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
     const long t256sq = static_cast<long>((m + 255) / 256) * ((n + 255) / 256) * batch;
     if (t256sq >= 256) variant = 15;       // falls back to 3 unless NN whole tiles
-    else if (t128 >= 256) variant = 13;    // falls back to 5
+    else if (t128 >= 256) variant = 16;    // falls back to 5
     else if (t256 >= 512) variant = 3;
     else variant = 0;
   }

@@ -339,6 +339,68 @@ __global__ __launch_bounds__(1024) void dwt_multi_kernel(
   for (int k = threadIdx.x; k < n; k += blockDim.x) orow[off + k] = in[k];
 }
 
+// Pyramid with compile-time filter length, 256 threads and LDS sized to the
+// signal (dynamic): several signals per CU instead of one 98 KB block.
+template <int ORDER>
+__global__ __launch_bounds__(256) void dwt_multi_t_kernel(
+    Taps taps, int ext, int levels, const float *__restrict__ src, int len,
+    float *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float dband[];
+  float hp[ORDER], lp[ORDER];
+#pragma unroll
+  for (int r = 0; r < ORDER; r++) {
+    hp[r] = taps.hp[r];
+    lp[r] = taps.lp[r];
+  }
+  const int64_t sig = blockIdx.x;
+  const float *x = src + sig * len;
+  float *orow = out + sig * len;
+  float *in = dband, *nxt = dband + len + ORDER;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) in[i] = x[i];
+  __syncthreads();
+  int n = len, off = 0;
+  for (int l = 0; l < levels; l++) {
+    const int half = n / 2;
+    for (int t = threadIdx.x; t < ORDER; t += blockDim.x) {
+      const int j = ext_index(n + t, n, ext);
+      in[n + t] = j < 0 ? 0.f : in[j];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < half; k += blockDim.x) {
+      float sh = 0.f, sl = 0.f;
+#pragma unroll
+      for (int j = 0; j < ORDER; j++) {
+        const float v = in[2 * k + j];
+        sh = fmaf(hp[j], v, sh);
+        sl = fmaf(lp[j], v, sl);
+      }
+      orow[off + k] = sh;
+      nxt[k] = sl;
+    }
+    __syncthreads();
+    float *t = in;  // the new low band becomes the input
+    in = nxt;
+    nxt = t;
+    off += half;
+    n = half;
+  }
+  for (int k = threadIdx.x; k < n; k += blockDim.x) orow[off + k] = in[k];
+}
+
+template <int ORDER>
+vs_status launch_dwt_multi_t(const Taps &t, int ext, int levels, const float *src, int len,
+                             float *out, int batch, hipStream_t s) {
+  const size_t lds = (2 * static_cast<size_t>(len) + 2 * ORDER) * sizeof(float);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(dwt_multi_t_kernel<ORDER>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (2 * kDwtMultiMax + 2 * 76) * 4);
+  VS_HIP(attr);
+  hipLaunchKernelGGL(dwt_multi_t_kernel<ORDER>, dim3(static_cast<unsigned>(batch)), dim3(256),
+                     lds, s, t, ext, levels, src, len, out);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
 vs_status launch_swt(const Taps &t, int level, int ext, const float *src,
                      int len, int64_t ss, float *hi, int64_t hs, float *lo,
                      int64_t ls, int batch, hipStream_t s) {
@@ -488,12 +550,45 @@ vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,
   VS_REQUIRE(src && out, "vs_dwt_multilevel: null pointer");
   VS_REQUIRE(levels >= 1 && len > 0 && len % (1 << levels) == 0,
              "vs_dwt_multilevel: length %d not divisible by 2^%d", len, levels);
-  VS_REQUIRE(len <= kDwtMultiMax, "vs_dwt_multilevel: length %d > %d", len,
-             kDwtMultiMax);
   VS_REQUIRE(batch >= 0, "vs_dwt_multilevel: negative batch");
   if (batch == 0) return VS_OK;
   Taps t;
   VS_TRY(make_taps(type, order, &t));
+  auto s = static_cast<hipStream_t>(stream);
+  if (len > kDwtMultiMax) {
+    // Long signals: level by level through HBM (vs_dwt), the band of level l
+    // feeding level l + 1; hi bands copied into the pyramid rows.
+    DeviceBuffer tmp;
+    const size_t rows = static_cast<size_t>(batch);
+    VS_TRY(tmp.alloc(2 * rows * static_cast<size_t>(len) * sizeof(float), s));
+    float *hbuf = tmp.as<float>(), *lbuf[2] = {hbuf + rows * (len / 2),
+                                               hbuf + rows * len + rows * (len / 4)};
+    const float *in = src;
+    int n = len, off = 0;
+    int64_t in_stride = len;
+    for (int l = 0; l < levels; l++) {
+      const int half = n / 2;
+      float *lo = lbuf[l & 1];
+      VS_TRY(vs_dwt(type, order, ext, in, n, in_stride, hbuf, lo, half, batch, stream));
+      VS_HIP(hipMemcpy2DAsync(out + off, len * sizeof(float), hbuf, half * sizeof(float),
+                              half * sizeof(float), rows, hipMemcpyDeviceToDevice, s));
+      in = lo;
+      in_stride = half;
+      off += half;
+      n = half;
+    }
+    VS_HIP(hipMemcpy2DAsync(out + off, len * sizeof(float), in, n * sizeof(float),
+                            n * sizeof(float), rows, hipMemcpyDeviceToDevice, s));
+    return VS_OK;
+  }
+  switch (order) {
+#define VS_DWT_T(O) \
+  case O: return launch_dwt_multi_t<O>(t, ext, levels, src, len, out, batch, s);
+    VS_DWT_T(2) VS_DWT_T(4) VS_DWT_T(6) VS_DWT_T(8) VS_DWT_T(12) VS_DWT_T(16) VS_DWT_T(18)
+    VS_DWT_T(20) VS_DWT_T(24) VS_DWT_T(30)
+#undef VS_DWT_T
+    default: break;
+  }
   const int threads = len / 2 >= 1024 ? 1024 : ((len / 2 + 63) / 64) * 64;
   hipLaunchKernelGGL(dwt_multi_kernel, dim3(static_cast<unsigned>(batch)),
                      dim3(threads), 0, static_cast<hipStream_t>(stream), t, ext,

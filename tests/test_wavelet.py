@@ -196,3 +196,26 @@ def test_multilevel_chain_via_recycle():
     rhi2, rlo2 = capi.wavelet_apply(D, 8, 0, lo1, na=True)
     np.testing.assert_allclose(hi2, rhi2, atol=5e-4)
     np.testing.assert_allclose(lo2, rlo2, atol=5e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("e", EXTS)
+def test_wavedec_long_signal_level_by_level(e):
+    """Signals longer than the LDS pyramid (16384) run level by level."""
+    import torch
+    from veles.simd_amd import ops
+    n = 1 << 15
+    x = torch.from_numpy((np.sin(np.arange(2 * n) * 0.001) * 10).astype(np.float32)).reshape(2, n)
+    pyr = ops.wavedec(x.cuda(), D, 8, levels=2, ext=e).cpu().numpy()
+    cur = x.numpy()
+    off = 0
+    for l in range(2):
+        m = cur.shape[1] // 2
+        nxt = np.zeros((2, m), np.float32)
+        for b in range(2):
+            vhi, vlo = capi.wavelet_apply(D, 8, e, cur[b], na=True)
+            np.testing.assert_allclose(pyr[b, off:off + m], vhi, atol=2e-3)
+            nxt[b] = vlo
+        cur = nxt
+        off += m
+    np.testing.assert_allclose(pyr[:, off:], cur, atol=2e-3)
