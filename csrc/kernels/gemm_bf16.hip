@@ -487,6 +487,143 @@ vs_status launch_glds(const Args &g, int batch, hipStream_t s) {
   return VS_OK;
 }
 
+// Three-stage LDS-DMA ring (as SGEMM generation 4, sgemm.hip): the DMA of
+// tile t+2 stays in flight across tile t's raw barrier; one __shared__ array
+// per stage and the k loop unrolled by three so the compiler can tell the
+// in-flight DMA from the stage being read (no vmcnt(0) drain); counted waits
+// through __builtin_amdgcn_s_waitcnt.
+template <int N>
+__device__ __forceinline__ void bf_wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 0xF) | ((N >> 4) << 14));
+}
+
+template <class C>
+__global__ __launch_bounds__(C::kThreads) void gemm_ring_kernel(Args g) {
+  __shared__ __attribute__((aligned(1024))) uint8_t r0[C::kStage];
+  __shared__ __attribute__((aligned(1024))) uint8_t r1[C::kStage];
+  __shared__ __attribute__((aligned(1024))) uint8_t r2[C::kStage];
+  constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
+  constexpr int kInstr = NI * (C::kInstrA + C::kInstrB);  // DMA per wave per tile
+  const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
+  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
+  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  unsigned tm, tn;
+  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
+  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
+  const int64_t kp = g.kp;
+  const uint16_t *A[2], *B[2];
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    A[i] = g.a[i] + blockIdx.z * g.sa;
+    B[i] = g.b[i] + blockIdx.z * g.sb;
+  }
+  float *Cp = g.c + blockIdx.z * g.sc;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int lrow = lane & 31, lh = lane >> 5;
+  const int arow = wm * (C::BM / C::WM) + lrow;
+  const int brow = wn * (C::BN / C::WN) + lrow;
+
+  auto stage = [&](uint8_t *base, int k0) {
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+      dma_image<C, C::kInstrA>(A[i], kp, m0, k0, base + i * C::kImgA, wid, lane);
+      dma_image<C, C::kInstrB>(B[i], kp, n0, k0, base + NI * C::kImgA + i * C::kImgB, wid,
+                               lane);
+    }
+  };
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+
+  auto compute = [&](const uint8_t *base) {
+#pragma unroll
+    for (int ks = 0; ks < C::BK / 16; ks++) {
+      const int c = 2 * ks + lh;
+      bf16x8 fa[NI][TM], fb[NI][TN];
+#pragma unroll
+      for (int i = 0; i < NI; i++) {
+#pragma unroll
+        for (int x = 0; x < TM; x++)
+          fa[i][x] = gfrag<C>(base + i * C::kImgA, arow + 32 * x, c);
+#pragma unroll
+        for (int y = 0; y < TN; y++)
+          fb[i][y] = gfrag<C>(base + NI * C::kImgA + i * C::kImgB, brow + 32 * y, c);
+      }
+#pragma unroll
+      for (int x = 0; x < TM; x++)
+#pragma unroll
+        for (int y = 0; y < TN; y++) {
+          if (C::TERMS == 3) {
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][x], fb[0][y],
+                                                                acc[x][y], 0, 0, 0);
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[1][y],
+                                                                acc[x][y], 0, 0, 0);
+          }
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[0][y],
+                                                              acc[x][y], 0, 0, 0);
+        }
+    }
+  };
+
+  const int nk = g.kp / C::BK;
+  stage(r0, 0);
+  if (nk > 1) stage(r1, C::BK);
+#define VS_RING_STEP(CUR, NEXT2)                             \
+  if (kt < nk) {                                             \
+    if (kt + 1 < nk) bf_wait_vmcnt<kInstr>();                \
+    else bf_wait_vmcnt<0>();                                 \
+    __builtin_amdgcn_s_barrier();                            \
+    if (kt + 2 < nk) stage(NEXT2, (kt + 2) * C::BK);         \
+    compute(CUR);                                            \
+  }                                                          \
+  kt++;
+  for (int kt = 0; kt < nk;) {
+    VS_RING_STEP(r0, r2)
+    VS_RING_STEP(r1, r0)
+    VS_RING_STEP(r2, r1)
+  }
+#undef VS_RING_STEP
+
+  const bool use_beta = g.beta != 0.f;
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      const int col = n0 + brow + 32 * y;
+      if (col >= g.n) continue;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int row = m0 + arow - lrow + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < g.m) {
+          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+          float v = g.alpha * acc[x][y][r];
+          if (use_beta) v += g.beta * *pc;
+          *pc = v;
+        }
+      }
+    }
+}
+
+template <class C>
+vs_status launch_ring(const Args &g, int batch, hipStream_t s) {
+  const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
+                                               ((g.n + C::BN - 1) / C::BN));
+  hipLaunchKernelGGL(gemm_ring_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
+                     dim3(C::kThreads), 0, s, g);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+using R1 = GCfg<1, 256, 128, 64, 4, 2>;   // bf16: 3 x 48 KiB stages, 8 waves of 64 x 64
+using R1S = GCfg<1, 256, 256, 32, 2, 4>;  // bf16: 3 x 32 KiB stages, 8 waves of 128 x 64
+using R3 = GCfg<3, 256, 128, 32, 4, 2>;   // bf16x3: 3 x 48 KiB stages
+
 using G1 = GCfg<1, 256, 256, 64, 2, 4>;   // bf16: 128 KiB LDS, 8 waves of 128 x 64
 using G3 = GCfg<3, 256, 128, 32, 4, 2>;   // bf16x3: 96 KiB LDS, 8 waves of 64 x 64
 
@@ -526,12 +663,20 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
     variant = t256 >= 256 ? 2 : (t256 >= 128 ? 1 : 0);
   }
-  VS_REQUIRE(variant >= 0 && variant <= 2, "gemm_bf16: unknown variant %d", variant);
+  VS_REQUIRE(variant >= 0 && variant <= 4, "gemm_bf16: unknown variant %d", variant);
   int bm = variant == 1 ? 256 : 128, bn = 128, bk = kBK;
   if (variant == 2) {
     bm = split ? G3::BM : G1::BM;
     bn = split ? G3::BN : G1::BN;
     bk = split ? G3::BK : G1::BK;
+  } else if (variant == 3 || (variant == 4 && split)) {
+    bm = split ? R3::BM : R1::BM;
+    bn = split ? R3::BN : R1::BN;
+    bk = split ? R3::BK : R1::BK;
+  } else if (variant == 4) {
+    bm = R1S::BM;
+    bn = R1S::BN;
+    bk = R1S::BK;
   }
   const int mp = (m + bm - 1) / bm * bm, np = (n + bn - 1) / bn * bn;
   const int kp = k == 0 ? bk : (k + bk - 1) / bk * bk;
@@ -563,6 +708,9 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   g.ldc = ldc;
   g.sc = sc;
   if (variant == 2) return split ? launch_glds<G3>(g, batch, s) : launch_glds<G1>(g, batch, s);
+  if (variant == 3 || (variant == 4 && split))
+    return split ? launch_ring<R3>(g, batch, s) : launch_ring<R1>(g, batch, s);
+  if (variant == 4) return launch_ring<R1S>(g, batch, s);
   if (split) return variant == 1 ? launch<C3L>(g, batch, s) : launch<C3>(g, batch, s);
   return variant == 1 ? launch<C1L>(g, batch, s) : launch<C1>(g, batch, s);
 }
@@ -581,6 +729,15 @@ vs_status vs_gemm_bf16(int ta, int tb, int m, int n, int k, float alpha, const u
   clear_error();
   return gbf::gemm_impl(false, ta, tb, m, n, k, alpha, a, lda, 0, b, ldb, 0, beta, c, ldc, 0, 1,
                         -1, static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_gemm_bf16_variant(int variant, int ta, int tb, int m, int n, int k, float alpha,
+                               const uint16_t *a, int64_t lda, const uint16_t *b,
+                               int64_t ldb, float beta, float *c, int64_t ldc,
+                               vs_stream_t stream) {
+  clear_error();
+  return gbf::gemm_impl(false, ta, tb, m, n, k, alpha, a, lda, 0, b, ldb, 0, beta, c, ldc, 0, 1,
+                        variant, static_cast<hipStream_t>(stream));
 }
 
 vs_status vs_gemm_bf16_strided_batched(int ta, int tb, int m, int n, int k, float alpha,

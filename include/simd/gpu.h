@@ -132,7 +132,8 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
 /// 6: 256x128x32, 7: 128x256x32; NN whole-tile LDS-DMA kernels (other shapes
 /// fall back to gen 1/2): gen 3 8: 256x128x32, 9: 128x128x32, 10: 256x256x16,
 /// 11/12: the 16x16x4-MFMA forms of 8/9; gen 4, three-stage DMA ring:
-/// 13: 128x128, 14: 256x128, 15: 256x256 (BK 16)).
+/// 13: 128x128, 14: 256x128, 15: 256x256 (BK 16); 16/17: 128x128 BK 32
+/// one wave per SIMD (asm / compiler fragment reads), 18: 256x128 BK 32).
 vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
                            int k, float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,
@@ -144,6 +145,13 @@ vs_status vs_gemm_bf16(int trans_a, int trans_b, int m, int n, int k,
                        float alpha, const uint16_t *a, int64_t lda,
                        const uint16_t *b, int64_t ldb, float beta, float *c,
                        int64_t ldc, vs_stream_t stream);
+/// Tuning entry point: explicit bf16 kernel variant (0: 128x128, 1: 256x128
+/// register-staged; 2: LDS-DMA 256x256 two-stage; 3: LDS-DMA three-stage
+/// ring 256x128 BK 64; 4: ring 256x256 BK 32; -1 auto).
+vs_status vs_gemm_bf16_variant(int variant, int trans_a, int trans_b, int m, int n,
+                               int k, float alpha, const uint16_t *a, int64_t lda,
+                               const uint16_t *b, int64_t ldb, float beta, float *c,
+                               int64_t ldc, vs_stream_t stream);
 vs_status vs_gemm_bf16_strided_batched(int trans_a, int trans_b, int m, int n,
                                        int k, float alpha, const uint16_t *a,
                                        int64_t lda, int64_t stride_a,

@@ -108,3 +108,30 @@ def test_large_shapes_use_lds_dma_kernel(ta, tb):
     c1 = ops.gemm_bf16(ah, bh, ta, tb)
     ref1 = (ah.double().T if ta else ah.double()) @ (bh.double().T if tb else bh.double())
     assert (c1.double() - ref1).abs().max().item() <= 2e-6 * k + 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_every_kernel_variant(variant):
+    """Each bf16 / bf16x3 kernel variant on a ragged shape, NN and TT."""
+    import ctypes
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    m, n, k = 1000, 700, 300
+    g = torch.Generator(device="cuda").manual_seed(variant)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for ta, tb in ((0, 0), (1, 1)):
+        a = torch.rand((k, m) if ta else (m, k), device="cuda", generator=g) * 2 - 1
+        b = torch.rand((n, k) if tb else (k, n), device="cuda", generator=g) * 2 - 1
+        c = torch.empty(m, n, device="cuda")
+        _lib.check(lib.vs_sgemm_bf16x3(ta, tb, m, n, k, 1.0, a.data_ptr(), a.shape[1],
+                                       b.data_ptr(), b.shape[1], 0.0, c.data_ptr(), n,
+                                       variant, s), "bf16x3")
+        ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
+        assert (c.double() - ref).abs().max().item() <= 8 * 2.0 ** -17 * math.sqrt(k) + 1e-6
+        ah, bh = a.bfloat16(), b.bfloat16()
+        _lib.check(lib.vs_gemm_bf16_variant(variant, ta, tb, m, n, k, 1.0, ah.data_ptr(),
+                                            ah.shape[1], bh.data_ptr(), bh.shape[1], 0.0,
+                                            c.data_ptr(), n, s), "bf16")
+        ref1 = (ah.double().T if ta else ah.double()) @ (bh.double().T if tb else bh.double())
+        assert (c.double() - ref1).abs().max().item() <= 2e-6 * k + 1e-6

@@ -32,15 +32,19 @@ def main():
         modes = {
             "exact": lambda: lib.vs_sgemm(0, 0, n, n, n, 1.0, a.data_ptr(), n, b.data_ptr(), n,
                                           0.0, c.data_ptr(), n, s),
-            "bf16x3_v0": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
-                                                     b.data_ptr(), n, 0.0, c.data_ptr(), n, 0, s),
-            "bf16x3_v1": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
-                                                     b.data_ptr(), n, 0.0, c.data_ptr(), n, 1, s),
             "bf16x3_v2": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
                                                      b.data_ptr(), n, 0.0, c.data_ptr(), n, 2, s),
+            "bf16x3_v3": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
+                                                     b.data_ptr(), n, 0.0, c.data_ptr(), n, 3, s),
             "bf16": lambda: lib.vs_gemm_bf16_strided_batched(0, 0, n, n, n, 1.0, ah.data_ptr(),
                                                              n, 0, bh.data_ptr(), n, 0, 0.0,
                                                              c.data_ptr(), n, 0, 1, s),
+            "bf16_v2": lambda: lib.vs_gemm_bf16_variant(2, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
+                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
+            "bf16_v3": lambda: lib.vs_gemm_bf16_variant(3, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
+                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
+            "bf16_v4": lambda: lib.vs_gemm_bf16_variant(4, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
+                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
             "torch_fp32": lambda: torch.matmul(a, b, out=c),
             "torch_bf16": lambda: torch.matmul(ah, bh),
         }

@@ -60,6 +60,8 @@ _SIGNATURES = {
                                       _vp]),
     "vs_gemm_bf16_strided_batched": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _i64, _vp,
                                           _i64, _i64, _f, _vp, _i64, _i64, _i, _vp]),
+    "vs_gemm_bf16_variant": (_i, [_i, _i, _i, _i, _i, _i, _f, _vp, _i64, _vp, _i64, _f,
+                                  _vp, _i64, _vp]),
     "vs_sgemm_bf16x3": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _vp, _i64, _f, _vp,
                              _i64, _i, _vp]),
     "vs_sgemm_bf16x3_strided_batched": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _i64,
