@@ -143,3 +143,42 @@ def test_sgemm_autograd():
     (a2 @ b2).sum().backward()
     torch.testing.assert_close(a.grad, a2.grad, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(b.grad, b2.grad, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", list(range(19)))
+def test_sgemm_every_variant(variant):
+    """Every SGEMM kernel variant (include/simd/gpu.h) on an aligned NN shape
+    (the LDS-DMA generations run only there) and on ragged / transposed shapes
+    (where they fall back), against float64."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g = torch.Generator(device="cuda").manual_seed(variant)
+    for (m, n, k, ta, tb) in [(512, 512, 256, 0, 0), (300, 257, 96, 0, 0), (256, 512, 64, 1, 1),
+                              (129, 70, 33, 0, 1)]:
+        a = torch.rand((k, m) if ta else (m, k), device="cuda", generator=g) - 0.5
+        b = torch.rand((n, k) if tb else (k, n), device="cuda", generator=g) - 0.5
+        c = torch.full((m, n), 3.0, device="cuda")
+        _lib.check(lib.vs_sgemm_variant(variant, ta, tb, m, n, k, 1.0, a.data_ptr(), a.shape[1],
+                                        b.data_ptr(), b.shape[1], 0.0, c.data_ptr(), n, s),
+                   "vs_sgemm_variant")
+        ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
+        assert (c.double() - ref).abs().max().item() < 1e-5 * k + 1e-5, (variant, m, n, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(2048, 2048, 512), (4096, 4096, 256)])
+def test_sgemm_default_large_paths(m, n, k):
+    """Default selection at the sizes that pick the three-stage LDS-DMA
+    kernels (gen 4), with beta accumulation."""
+    import torch
+    from veles.simd_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(m + k)
+    a = torch.rand(m, k, device="cuda", generator=g) * 2 - 1
+    b = torch.rand(k, n, device="cuda", generator=g) * 2 - 1
+    c = ops.sgemm(a, b)
+    ref = a.double() @ b.double()
+    assert (c.double() - ref).abs().max().item() < 2e-6 * k
