@@ -176,3 +176,29 @@ def test_rccl_backend_one_rank_per_device():
         a = np.random.default_rng(1).standard_normal((2, 64, 32)).astype(np.float32)
         b = np.random.default_rng(2).standard_normal((2, 32, 48)).astype(np.float32)
         np.testing.assert_allclose(g.sgemm_rowsplit(a, b), a @ b, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_watchdog_timeout_aborts_context():
+    """Failure detection: vs_dist_synchronize gives up after the timeout with
+    VS_ERR_TIMEOUT (status 7) and the context refuses further work."""
+    import ctypes
+    import torch
+    lib = _lib.lib()
+    g = native.DeviceGroup(1, devices=[0], backend="local", timeout_ms=1)
+    # ~1 s of GEMMs queued on the rank's stream, then a 1 ms watchdog
+    n = 8192
+    a = torch.rand(n, n, device="cuda")
+    c = torch.empty(n, n, device="cuda")
+    stream = ctypes.c_void_p(g.stream(0))
+    for _ in range(100):
+        _lib.check(lib.vs_sgemm(0, 0, n, n, n, 1.0, ctypes.c_void_p(a.data_ptr()), n,
+                                ctypes.c_void_p(a.data_ptr()), n, 0.0,
+                                ctypes.c_void_p(c.data_ptr()), n, stream), "vs_sgemm")
+    with pytest.raises(_lib.VelesError, match="status 7"):
+        g.synchronize()
+    with pytest.raises(_lib.VelesError, match="aborted"):
+        g.broadcast([c[0]])
+    torch.cuda.synchronize()  # drain the queued work before the process moves on
+    lib.vs_stream_synchronize(stream)
+    g.close()
