@@ -49,6 +49,24 @@ constexpr int kDirX = kDirOut + kDirTaps;              // x window (+1 spare)
 
 __device__ __forceinline__ int xpad(int i) { return i + (i >> 5); }
 
+// Each lane holds 8 consecutive outputs; written straight out, a wave's store
+// instruction would touch 64 separate 32-byte pieces.  Bounce them through
+// the (reused) LDS window so every store instruction writes 256 consecutive
+// bytes per wave.  `buf` must hold kDirOut floats.
+__device__ __forceinline__ void store_outputs(const float (&acc)[kDirPerThread], float *buf,
+                                              float *__restrict__ yrow, int n0, int q0,
+                                              int ylen) {
+  __syncthreads();  // every lane is done reading the window
+#pragma unroll
+  for (int r = 0; r < kDirPerThread; r++) buf[q0 + r] = acc[r];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kDirPerThread; k++) {
+    const int i = threadIdx.x + k * kDirThreads;
+    if (n0 + i < ylen) yrow[n0 + i] = buf[i];
+  }
+}
+
 __global__ __launch_bounds__(kDirThreads) void direct_kernel(
     const float *__restrict__ x, int xlen, int64_t xs, const float *__restrict__ h,
     int hlen, int64_t hs, float *__restrict__ y, int64_t ys, int ylen,
@@ -100,12 +118,54 @@ __global__ __launch_bounds__(kDirThreads) void direct_kernel(
       for (int r = 0; r < kDirPerThread; r++) w[kDirPerThread + r] = w[r];
     }
   }
-  float *yrow = y + sig * ys;
+  store_outputs(acc, sx, y + sig * ys, n0, q0, ylen);
+}
+
+// Short filters (h <= HM): taps in registers (zero-padded to HM), the x
+// window of the block staged once in LDS, each lane reads its 8 + HM - 1
+// window samples with 16-byte LDS reads.  Memory-bound: one pass over x and y.
+template <int HM>
+__global__ __launch_bounds__(kDirThreads) void direct_small_kernel(
+    const float *__restrict__ x, int xlen, int64_t xs, const float *__restrict__ h,
+    int hlen, int64_t hs, float *__restrict__ y, int64_t ys, int ylen, int reverse) {
+  constexpr int W = kDirOut + HM + 8;  // window floats (+ slack for the b128 reads)
+  __shared__ __attribute__((aligned(16))) float sx[W];
+  const int sig = blockIdx.y;
+  const float *xrow = x + sig * xs;
+  const float *hrow = h + sig * hs;
+  const int n0 = blockIdx.x * kDirOut;
+  // window: sx[i] = x[n0 - (HM - 1) + i]
+  const int xbase = n0 - (HM - 1);
+  for (int i = threadIdx.x; i < W; i += kDirThreads) {
+    const int p = xbase + i;
+    sx[i] = (p >= 0 && p < xlen) ? xrow[p] : 0.f;
+  }
+  float tap[HM];
+#pragma unroll
+  for (int m = 0; m < HM; m++)
+    tap[m] = m < hlen ? (reverse ? hrow[hlen - 1 - m] : hrow[m]) : 0.f;
+  __syncthreads();
+  const int q0 = threadIdx.x * kDirPerThread;
+  constexpr int NW = (kDirPerThread + HM - 1 + 3) / 4;  // float4 reads per lane
+  float w[4 * NW];
+#pragma unroll
+  for (int c = 0; c < NW; c++) {
+    const float4 v = *reinterpret_cast<const float4 *>(sx + q0 + 4 * c);
+    w[4 * c] = v.x;
+    w[4 * c + 1] = v.y;
+    w[4 * c + 2] = v.z;
+    w[4 * c + 3] = v.w;
+  }
+  // y[n0 + q0 + r] = sum_m tap[m] x[n0 + q0 + r - m] = sum_m tap[m] w[r - m + HM - 1]
+  float acc[kDirPerThread];
 #pragma unroll
   for (int r = 0; r < kDirPerThread; r++) {
-    const int n = n0 + q0 + r;
-    if (n < ylen) yrow[n] = acc[r];
+    float a = 0.f;
+#pragma unroll
+    for (int m = 0; m < HM; m++) a = fmaf(tap[m], w[r - m + HM - 1], a);
+    acc[r] = a;
   }
+  store_outputs(acc, sx, y + sig * ys, n0, q0, ylen);
 }
 
 // ------------------------------------------------------ filter spectrum
@@ -295,8 +355,18 @@ vs_status run_direct(int correlate, const float *x, int xlen, int64_t xs,
   const int ylen = xlen + hlen - 1;
   const dim3 grid(static_cast<unsigned>((ylen + kDirOut - 1) / kDirOut),
                   static_cast<unsigned>(batch));
-  hipLaunchKernelGGL(direct_kernel, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
-                     hlen, hs, y, ys, ylen, correlate);
+  if (hlen <= 8)
+    hipLaunchKernelGGL(direct_small_kernel<8>, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
+                       hlen, hs, y, ys, ylen, correlate);
+  else if (hlen <= 16)
+    hipLaunchKernelGGL(direct_small_kernel<16>, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
+                       hlen, hs, y, ys, ylen, correlate);
+  else if (hlen <= 32)
+    hipLaunchKernelGGL(direct_small_kernel<32>, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
+                       hlen, hs, y, ys, ylen, correlate);
+  else
+    hipLaunchKernelGGL(direct_kernel, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
+                       hlen, hs, y, ys, ylen, correlate);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }

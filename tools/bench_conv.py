@@ -23,12 +23,13 @@ def main():
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     x = torch.randn(batch, xlen, device="cuda")
     res = {}
-    for hlen in [16, 64, 512, 4096]:
+    hlens = [int(v) for v in os.environ.get("HLENS", "16,64,512,4096").split(",")]
+    for hlen in hlens:
         h = torch.randn(hlen, device="cuda")
         ylen = xlen + hlen - 1
         y = torch.empty(batch, ylen, device="cuda")
         variants = [("auto", 0, 14), ("direct", 1, 14), ("fft", 2, 14)]
-        variants += [(f"os{lg}", 3, lg) for lg in (11, 12, 13, 14) if (1 << lg) > hlen + 64]
+        variants += [(f"os{lg}", 3, lg) for lg in (11, 12, 13, 14) if (1 << lg) > 2 * hlen + 64]
         times = {v[0]: [] for v in variants}
         ev0, ev1 = torch.cuda.Event(True), torch.cuda.Event(True)
         for r in range(rounds):
