@@ -1112,6 +1112,253 @@ bool launch_cfg4(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipStre
   return true;
 }
 
+// Generation 5: generation 4's three-stage LDS-DMA ring with the whole k loop
+// software-pipelined by hand.  Gen 4 lost ~10 % of the MFMA cycles at tile
+// boundaries: every wave of a block reached the barrier at the same moment,
+// then all of them issued their fragment reads and waited for them, and the
+// MFMA pipe ran dry in between (SQ_VALU_MFMA_BUSY 0.905 of 4 x SQ_BUSY_CU at
+// 4096^3 against hipBLASLt's 0.978, profiles/r1/pmc_v15_summary.md).  Here
+// the barrier sits in the MIDDLE of a tile's MFMA stream:
+//
+//   tile t:  MFMA k-steps 0,1 from registers R[t&1]
+//            wait own DMA of tile t+1 (counted vmcnt) ; s_barrier
+//            DMA tile t+3 into tile t's stage (free: its reads all retired)
+//            MFMA k-steps 2,3 from R[t&1], one fragment read of tile t+1
+//            into R[(t+1)&1] issued after each MFMA
+//
+// so the reads of the next tile overlap the MFMAs of this one and the next
+// tile starts with its fragments already in registers.  MFMAs and fragment
+// reads are inline asm (volatile asm keeps program order; the compiler only
+// allocates registers), so the interleave is exactly as written; the
+// hazards the compiler would otherwise cover are handled explicitly
+// (s_nop after the VALU zeroing of the accumulators and before the
+// epilogue reads them).  Three stages give each DMA two tiles of cover.
+// The dynamic LDS size is padded to kLdsBytes so that exactly the intended
+// number of blocks shares a CU.
+template <int BM_, int BN_, int WM_, int WN_, int LDS_KB_ = 0, bool AGPR_ = false>
+struct Cfg5 {
+  static constexpr int BM = BM_, BN = BN_, BK = 16, WM = WM_, WN = WN_;
+  // accumulators in AGPRs (MFMA srcC/vdst may be AGPRs): frees the 256
+  // architectural VGPRs for fragments when a wave owns a 128 x 128 tile
+  static constexpr bool AGPR = AGPR_;
+  static constexpr int kThreads = 64 * WM * WN, kWaves = WM * WN;
+  static constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  static constexpr int RBA = BK * 4, RBB = BN * 4;
+  static constexpr int kImgA = BM * RBA, kImgB = BK * RBB, kStage = kImgA + kImgB;
+  static constexpr int kLdsBytes = 3 * kStage > LDS_KB_ * 1024 ? 3 * kStage : LDS_KB_ * 1024;
+  static constexpr int kInstrA = kImgA / 1024 / kWaves, kInstrB = kImgB / 1024 / kWaves;
+  static constexpr int kInstr = kInstrA + kInstrB;
+  static_assert(kInstrA * 1024 * kWaves == kImgA && kInstrB * 1024 * kWaves == kImgB,
+                "tile not divisible into whole DMA instructions per wave");
+  static_assert(2 * kInstr < 64, "vmcnt immediates");
+  static_assert(TM + 4 * TN <= 2 * TM * TN, "fragment reads must fit between the MFMAs");
+};
+
+#define VS_MFMA_16X16X4(ACC, A, B) \
+  asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(ACC) : "v"(A), "v"(B))
+#define VS_MFMA_16X16X4_AGPR(ACC, A, B) \
+  asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(ACC) : "v"(A), "v"(B))
+
+template <class C>
+struct Gen5 {
+  static constexpr int TM = C::TM, TN = C::TN;
+  static constexpr int kReads = TM + 4 * TN;
+  struct Frag {
+    float4 a[TM];
+    float b[TN][4];
+  };
+
+  // fragment read r of a tile: A rows first (ds_read_b128: 4 k of one row),
+  // then B (ds_read_b32, one k of one column)
+  template <int R>
+  __device__ __forceinline__ static void read(Frag &f, uint32_t va, const uint32_t (&vb)[TN]) {
+    if constexpr (R < TM) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f.a[R]) : "v"(va), "i"(1024 * R)
+                   : "memory");
+    } else {
+      constexpr int y = (R - TM) / 4, s = (R - TM) % 4;
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(f.b[y][s]) : "v"(vb[y]),
+                   "i"(4 * s * C::BN) : "memory");
+    }
+  }
+
+  template <int R = 0>
+  __device__ __forceinline__ static void read_all(Frag &f, uint32_t va,
+                                                  const uint32_t (&vb)[TN]) {
+    if constexpr (R < kReads) {
+      read<R>(f, va, vb);
+      read_all<R + 1>(f, va, vb);
+    }
+  }
+
+  // MFMAs number I .. (end of k-steps S0, S0+1); when NEXT is set the
+  // fragment read I - I0 of the next tile follows MFMA I
+  template <int S0, bool NEXT, int I = 0>
+  __device__ __forceinline__ static void mfma_half(floatx4 (&acc)[TM][TN], const Frag &f,
+                                                   Frag &nf, uint32_t va,
+                                                   const uint32_t (&vb)[TN]) {
+    if constexpr (I < 2 * TM * TN) {
+      constexpr int s = S0 + I / (TM * TN), x = (I / TN) % TM, y = I % TN;
+      if constexpr (C::AGPR) VS_MFMA_16X16X4_AGPR(acc[x][y], comp(f.a[x], s), f.b[y][s]);
+      else VS_MFMA_16X16X4(acc[x][y], comp(f.a[x], s), f.b[y][s]);
+      if constexpr (NEXT && I < kReads) read<I>(nf, va, vb);
+      mfma_half<S0, NEXT, I + 1>(acc, f, nf, va, vb);
+    }
+  }
+};
+
+template <class C>
+__global__ __launch_bounds__(C::kThreads) void sgemm5_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(1024))) uint8_t smem5[];
+  using K = Gen5<C>;
+  constexpr int TM = C::TM, TN = C::TN;
+  const unsigned tiles_n = g.n / C::BN, tiles_m = g.m / C::BM;
+  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  unsigned tm, tn;
+  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
+  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
+  const float *A = g.a + blockIdx.z * g.stride_a;
+  const float *B = g.b + blockIdx.z * g.stride_b;
+  float *Cp = g.c + blockIdx.z * g.stride_c;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int arow = wm * (C::BM / C::WM) + l16;
+  const int bcol = wn * (C::BN / C::WN) + l16;
+
+  // fragment byte offsets inside a stage (see Gen4::group for the layouts):
+  // A rows 16x apart differ by 1024 B (the swizzle only depends on row bit 3),
+  // B k-steps s differ by 4 * BN B; both go in the instruction's offset field
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem5));
+  const uint32_t aoff = arow * C::RBA + 16 * aswz4(arow, q);
+  uint32_t boff[TN];
+#pragma unroll
+  for (int y = 0; y < TN; y++) {
+    const int col = bcol + 16 * y;
+    boff[y] = C::kImgA + 16 * q * C::BN + 4 * (col & 3) + 16 * ((col >> 2) ^ ((q & 1) << 2));
+  }
+  // DMA sources for k = 0 (same per-lane mapping as Gen4::stage)
+  const float *pa[C::kInstrA];
+  const float *pb[C::kInstrB];
+#pragma unroll
+  for (int i = 0; i < C::kInstrA; i++) {
+    const int row = (wid * C::kInstrA + i) * (1024 / C::RBA) + lane / 4;
+    pa[i] = A + static_cast<int64_t>(m0 + row) * g.lda + 4 * aswz4(row, lane % 4);
+  }
+#pragma unroll
+  for (int i = 0; i < C::kInstrB; i++) {
+    const int byte = (wid * C::kInstrB + i) * 1024 + lane * 16;
+    const int kr = byte / C::RBB, pcn = (byte % C::RBB) / 16;
+    pb[i] = B + static_cast<int64_t>(kr) * g.ldb + n0 + 4 * (pcn ^ (((kr >> 2) & 1) << 2));
+  }
+  const auto dma = [&](int st, int kt) {
+    uint8_t *base = smem5 + st * C::kStage;
+#pragma unroll
+    for (int i = 0; i < C::kInstrA; i++)
+      __builtin_amdgcn_global_load_lds((glob_void_t *)(pa[i] + kt * C::BK),
+                                       (lds_void_t *)(base + (wid * C::kInstrA + i) * 1024),
+                                       16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < C::kInstrB; i++)
+      __builtin_amdgcn_global_load_lds(
+          (glob_void_t *)(pb[i] + static_cast<int64_t>(kt) * C::BK * g.ldb),
+          (lds_void_t *)(base + C::kImgA + (wid * C::kInstrB + i) * 1024), 16, 0, 0);
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      acc[x][y] = floatx4{0.f, 0.f, 0.f, 0.f};
+      // materialise before the s_nop below
+      if constexpr (C::AGPR) asm volatile("" : "+a"(acc[x][y]));
+      else asm volatile("" : "+v"(acc[x][y]));
+    }
+  asm volatile("s_nop 7" ::: "memory");  // VALU write -> MFMA srcC read
+
+  const int nk = g.k / C::BK;
+  dma(0, 0);
+  if (nk > 1) dma(1, 1);
+  if (nk > 2) dma(2, 2);
+  if (nk > 2) wait_vmcnt<2 * C::kInstr>();
+  else if (nk > 1) wait_vmcnt<C::kInstr>();
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  typename K::Frag f0, f1;
+  uint32_t vb[TN];
+#pragma unroll
+  for (int y = 0; y < TN; y++) vb[y] = lds0 + boff[y];
+  K::read_all(f0, lds0 + aoff, vb);
+
+  // tile kt: stage kt % 3, registers f[kt & 1].  The MFMA stream is straight
+  // line (no branch around it: with one, the register coalescer split the
+  // accumulators and copied them at every tile); the last tile's reads of
+  // the "next" tile fetch a stale stage and are never used.
+#define VS_GEN5_STEP(CUR, NXT)                                                  \
+  {                                                                             \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                          \
+    K::template mfma_half<0, false>(acc, CUR, NXT, 0u, vb);                     \
+    if (kt + 2 < nk) wait_vmcnt<C::kInstr>();                                   \
+    else wait_vmcnt<0>();                                                       \
+    __builtin_amdgcn_s_barrier();                                               \
+    if (kt + 3 < nk) dma(sc, kt + 3);                                           \
+    sc = sc == 2 ? 0 : sc + 1;                                                  \
+    const uint32_t sb = lds0 + sc * C::kStage;                                  \
+    _Pragma("unroll") for (int y = 0; y < TN; y++) vb[y] = sb + boff[y];        \
+    K::template mfma_half<2, true>(acc, CUR, NXT, sb + aoff, vb);               \
+    kt++;                                                                       \
+  }
+  int sc = 0;  // stage of tile kt
+  for (int kt = 0; kt < nk;) {
+    VS_GEN5_STEP(f0, f1)
+    if (kt < nk) VS_GEN5_STEP(f1, f0)
+  }
+#undef VS_GEN5_STEP
+
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> VALU read
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      if constexpr (C::AGPR) asm volatile("" : "+a"(acc[x][y]));
+      else asm volatile("" : "+v"(acc[x][y]));
+    }
+  const bool use_beta = g.beta != 0.f;
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      const int col = n0 + bcol + 16 * y;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = m0 + arow - l16 + 16 * x + 4 * q + r;
+        float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+        float v = g.alpha * acc[x][y][r];
+        if (use_beta) v += g.beta * *pc;
+        *pc = v;
+      }
+    }
+}
+
+template <class C>
+bool launch_cfg5(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipStream_t s) {
+  if (ta || tb || !vec || g.m % C::BM || g.n % C::BN || g.k % C::BK || g.k == 0) return false;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&sgemm5_kernel<C>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);
+  const unsigned tiles = static_cast<unsigned>((g.m / C::BM) * (g.n / C::BN));
+  hipLaunchKernelGGL(sgemm5_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
+                     dim3(C::kThreads), C::kLdsBytes, s, g);
+  return true;
+}
+
+using Cfg5A = Cfg5<128, 128, 2, 2, 56>;  // 4 waves of 64 x 64; LDS padded: 2 blocks / CU
+using Cfg5B = Cfg5<256, 128, 2, 2, 56>;  // 4 waves of 128 x 64 (128 accumulator VGPRs)
+using Cfg5C = Cfg5<128, 128, 2, 2>;      // 48 KiB: up to 3 blocks / CU
+using Cfg5D = Cfg5<256, 256, 2, 2, 0, true>;    // 4 waves of 128 x 128, AGPR accumulators
+using Cfg5E = Cfg5<256, 128, 2, 2, 56, true>;   // Cfg5B with AGPR accumulators
+
 using Cfg4A = Cfg4<128, 128, 2, 2, false>;  // 48 KiB LDS (3 stages), 4 waves of 64 x 64
 using Cfg4B = Cfg4<256, 128, 4, 2>;   // 72 KiB LDS, 8 waves of 64 x 64
 using Cfg4C = Cfg4<256, 256, 4, 4, false>;  // 96 KiB LDS, 16 waves of 64 x 64
@@ -1213,6 +1460,21 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
       break;
     case 18:
       if (!launch_cfg4<Cfg4G>(g, ta, tb, vec, batch, s)) launch_cfg<CfgC>(g, ta, tb, vec, batch, s);
+      break;
+    case 19:
+      if (!launch_cfg5<Cfg5A>(g, ta, tb, vec, batch, s)) launch_cfg2<Cfg2A>(g, ta, tb, vec, batch, s);
+      break;
+    case 20:
+      if (!launch_cfg5<Cfg5B>(g, ta, tb, vec, batch, s)) launch_cfg<CfgC>(g, ta, tb, vec, batch, s);
+      break;
+    case 21:
+      if (!launch_cfg5<Cfg5C>(g, ta, tb, vec, batch, s)) launch_cfg2<Cfg2A>(g, ta, tb, vec, batch, s);
+      break;
+    case 22:
+      if (!launch_cfg5<Cfg5D>(g, ta, tb, vec, batch, s)) launch_cfg<CfgC>(g, ta, tb, vec, batch, s);
+      break;
+    case 23:
+      if (!launch_cfg5<Cfg5E>(g, ta, tb, vec, batch, s)) launch_cfg<CfgC>(g, ta, tb, vec, batch, s);
       break;
 
     default:

@@ -133,7 +133,11 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
 /// fall back to gen 1/2): gen 3 8: 256x128x32, 9: 128x128x32, 10: 256x256x16,
 /// 11/12: the 16x16x4-MFMA forms of 8/9; gen 4, three-stage DMA ring:
 /// 13: 128x128, 14: 256x128, 15: 256x256 (BK 16); 16/17: 128x128 BK 32
-/// one wave per SIMD (asm / compiler fragment reads), 18: 256x128 BK 32).
+/// one wave per SIMD (asm / compiler fragment reads), 18: 256x128 BK 32;
+/// gen 5, hand-pipelined (barrier mid-tile, next tile's fragment reads
+/// interleaved with this tile's MFMAs): 19: 128x128 (2 blocks / CU),
+/// 20: 256x128 (waves of 128x64), 21: 128x128 (3 blocks / CU), 22: 256x256
+/// (waves of 128x128, AGPR accumulators), 23: variant 20 with AGPR accumulators).
 vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
                            int k, float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,

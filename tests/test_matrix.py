@@ -146,7 +146,7 @@ def test_sgemm_autograd():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", list(range(19)))
+@pytest.mark.parametrize("variant", list(range(24)))
 def test_sgemm_every_variant(variant):
     """Every SGEMM kernel variant (include/simd/gpu.h) on an aligned NN shape
     (the LDS-DMA generations run only there) and on ragged / transposed shapes
@@ -167,6 +167,28 @@ def test_sgemm_every_variant(variant):
                    "vs_sgemm_variant")
         ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
         assert (c.double() - ref).abs().max().item() < 1e-5 * k + 1e-5, (variant, m, n, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [13, 15, 19, 20, 22, 23])
+@pytest.mark.parametrize("k", [16, 32, 48, 64, 80, 4096])
+def test_sgemm_pipeline_depths(variant, k):
+    """The LDS-DMA rings at every pipeline depth: 1, 2, 3 and more k tiles
+    (prologue / drain paths of the counted-vmcnt schedule), beta != 0."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g = torch.Generator(device="cuda").manual_seed(k)
+    m, n = 512, 256
+    a = torch.rand(m, k, device="cuda", generator=g) - 0.5
+    b = torch.rand(k, n, device="cuda", generator=g) - 0.5
+    c = torch.rand(m, n, device="cuda", generator=g)
+    ref = 0.5 * (a.double() @ b.double()) + 2.0 * c.double()
+    _lib.check(lib.vs_sgemm_variant(variant, 0, 0, m, n, k, 0.5, a.data_ptr(), k, b.data_ptr(),
+                                    n, 2.0, c.data_ptr(), n, s), "vs_sgemm_variant")
+    assert (c.double() - ref).abs().max().item() < 1e-5 * k + 1e-5, (variant, k)
 
 
 @pytest.mark.gpu
