@@ -34,6 +34,7 @@
 
 namespace vs {
 namespace conv {
+extern int g_conv_buf;  // tuning knobs, defined below
 namespace {
 
 using fft::cmul;
@@ -202,70 +203,167 @@ struct BlockArgs {
   float scale;
 };
 
-template <int LOGN>
-__global__ __launch_bounds__(Plan<LOGN>::TPS) void block_conv_kernel(
-    BlockArgs a, const float2 *__restrict__ tw) {
-  using PL = Plan<LOGN>;
-  __shared__ float2 lds[PL::kLds];
-  const int t = threadIdx.x;
-  const long long s0 = 2LL * blockIdx.x, s1 = s0 + 1;
-  const long long sig0 = s0 / a.nblk, sig1 = s1 / a.nblk;
-  const int b0 = static_cast<int>(s0 % a.nblk), b1 = static_cast<int>(s1 % a.nblk);
-  const bool ok0 = b0 * static_cast<long long>(a.step) < a.ylen;
-  const bool ok1 = s1 < a.nslots && b1 * static_cast<long long>(a.step) < a.ylen;
-  const float *x0 = a.x + sig0 * a.xs;
-  const float *x1 = a.x + sig1 * a.xs;
-  const int st0 = b0 * a.step - a.pre, st1 = b1 * a.step - a.pre;
+// Block pair p = slots 2p and 2p + 1 (the real and imaginary part of one
+// complex transform).  Rows of slots that do not exist (past the last
+// signal / past the output) are redirected to row 0 so every load address is
+// valid; their samples are zeroed and their outputs not stored.
+struct PairPos {
+  long long sig0, sig1;
+  int b0, b1;
+  bool ok0, ok1;
+};
 
-  float2 v[PL::E];
+__device__ __forceinline__ PairPos pair_pos(const BlockArgs &a, long long p) {
+  PairPos q;
+  const long long s0 = 2 * p, s1 = s0 + 1;
+  q.sig0 = s0 / a.nblk;
+  q.sig1 = s1 / a.nblk;
+  q.b0 = static_cast<int>(s0 - q.sig0 * a.nblk);
+  q.b1 = static_cast<int>(s1 - q.sig1 * a.nblk);
+  q.ok0 = q.b0 * static_cast<long long>(a.step) < a.ylen;
+  q.ok1 = s1 < a.nslots && q.b1 * static_cast<long long>(a.step) < a.ylen;
+  return q;
+}
+
+// Inputs of the pair in the first pass's register pattern.  BUF: raw buffer
+// loads through one descriptor per slot -- the hardware range check returns
+// 0 for samples before / past the row and for a slot that does not exist
+// (zero records), so the loads need no select and can all be in flight
+// before the first butterfly (a select per element made hipcc wait for each
+// load group before issuing the next).  !BUF (rows of 2^29 samples or more,
+// beyond a 32-bit byte offset): clamped flat loads, zeroed afterwards.
+template <class PL, bool BUF>
+__device__ __forceinline__ void load_pair(const BlockArgs &a, const PairPos &q, int t,
+                                          float2 (&v)[PL::E]) {
+  const float *x0 = a.x + (q.ok0 ? q.sig0 : 0) * a.xs;
+  const float *x1 = a.x + (q.ok1 ? q.sig1 : 0) * a.xs;
+  const int st0 = q.b0 * a.step - a.pre, st1 = q.b1 * a.step - a.pre;
   constexpr int R0 = PL::first_radix(false);
+  // buffer loads only from non-negative offsets: the first block of a
+  // signal (history before sample 0) takes the flat path
+  if (BUF && st0 >= 0 && st1 >= 0) {
+    const auto r0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x0), 0,
+                                                      q.ok0 ? 4 * a.xlen : 0, 0x00020000);
+    const auto r1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x1), 0,
+                                                      q.ok1 ? 4 * a.xlen : 0, 0x00020000);
+    const int o0 = 4 * (st0 + t), o1 = 4 * (st1 + t);
 #pragma unroll
-  for (int b = 0; b < PL::E / R0; b++)
+    for (int b = 0; b < PL::E / R0; b++)
 #pragma unroll
-    for (int j = 0; j < R0; j++) {
-      const int n = reg_index<PL, R0>(t, b, j);
-      const int p0 = st0 + n, p1 = st1 + n;
-      v[b * R0 + j] =
-          make_float2(ok0 && p0 >= 0 && p0 < a.xlen ? x0[p0] : 0.f,
-                      ok1 && p1 >= 0 && p1 < a.xlen ? x1[p1] : 0.f);
-    }
-  fft::transform<PL, false, false>(v, lds, t, tw);
+      for (int j = 0; j < R0; j++) {
+        const int d = 4 * (reg_index<PL, R0>(0, b, j));
+        // (the b32 builtins move raw bits: uint32)
+        v[b * R0 + j] =
+            make_float2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r0, o0 + d, 0, 0)),
+                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r1, o1 + d, 0, 0)));
+      }
+  } else {
+    const int last = a.xlen - 1;
+#pragma unroll
+    for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+      for (int j = 0; j < R0; j++) {
+        const int n = reg_index<PL, R0>(t, b, j);
+        const int p0 = st0 + n, p1 = st1 + n;
+        const float u0 = x0[min(max(p0, 0), last)];
+        const float u1 = x1[min(max(p1, 0), last)];
+        v[b * R0 + j] =
+            make_float2(q.ok0 && static_cast<unsigned>(p0) <= static_cast<unsigned>(last) ? u0 : 0.f,
+                        q.ok1 && static_cast<unsigned>(p1) <= static_cast<unsigned>(last) ? u1 : 0.f);
+      }
+  }
+}
 
-  // Multiply by the filter spectrum (both slots share it).
-  const float2 *H = a.H + (a.h_per_signal ? sig0 * PL::N : 0);
+// Multiply by the filter spectrum (both slots share it).
+template <class PL>
+__device__ __forceinline__ void mul_spectrum(const BlockArgs &a, const PairPos &q, int t,
+                                             float2 (&v)[PL::E]) {
+  const float2 *H = a.H + (a.h_per_signal ? q.sig0 * PL::N : 0);
   constexpr int RL = PL::last_radix(false);
 #pragma unroll
   for (int b = 0; b < PL::E / RL; b++)
 #pragma unroll
     for (int j = 0; j < RL; j++)
       v[b * RL + j] = cmul(v[b * RL + j], H[reg_index<PL, RL>(t, b, j)]);
+}
 
-  __syncthreads();  // LDS reuse by the inverse transform
+// The `step` valid outputs of each slot, from the inverse transform's last
+// pass (the first radix of the forward plan).  BUF: buffer stores whose range
+// check drops outputs past the row and every store of a missing slot.
+template <class PL, bool BUF>
+__device__ __forceinline__ void store_pair(const BlockArgs &a, const PairPos &q, int t,
+                                           const float2 (&v)[PL::E]) {
+  constexpr int RI = PL::radix(0);
+  float *y0 = a.y + (q.ok0 ? q.sig0 : 0) * a.ys;
+  float *y1 = a.y + (q.ok1 ? q.sig1 : 0) * a.ys;
+  const int base0 = q.b0 * a.step - a.pre, base1 = q.b1 * a.step - a.pre;
+  if constexpr (BUF) {
+    const auto w0 = __builtin_amdgcn_make_buffer_rsrc(y0, 0, q.ok0 ? 4 * a.ylen : 0, 0x00020000);
+    const auto w1 = __builtin_amdgcn_make_buffer_rsrc(y1, 0, q.ok1 ? 4 * a.ylen : 0, 0x00020000);
+#pragma unroll
+    for (int b = 0; b < PL::E / RI; b++)
+#pragma unroll
+      for (int j = 0; j < RI; j++) {
+        const int n = reg_index<PL, RI>(t, b, j) - a.pre;
+        if (n < 0 || n >= a.step) continue;
+        const float2 r = v[b * RI + j];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x * a.scale), w0,
+                                              4 * (base0 + a.pre + n), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y * a.scale), w1,
+                                              4 * (base1 + a.pre + n), 0, 0);
+      }
+  } else {
+#pragma unroll
+    for (int b = 0; b < PL::E / RI; b++)
+#pragma unroll
+      for (int j = 0; j < RI; j++) {
+        const int n = reg_index<PL, RI>(t, b, j) - a.pre;
+        if (n < 0 || n >= a.step) continue;
+        const float2 r = v[b * RI + j];
+        const long long o0 = static_cast<long long>(q.b0) * a.step + n;
+        const long long o1 = static_cast<long long>(q.b1) * a.step + n;
+        if (q.ok0 && o0 < a.ylen) y0[o0] = r.x * a.scale;
+        if (q.ok1 && o1 < a.ylen) y1[o1] = r.y * a.scale;
+      }
+  }
+}
+
+// One workgroup per block pair.  No barrier between the transforms: the
+// forward transform's last LDS read is followed by a barrier inside it.
+template <int LOGN, bool BUF>
+__global__ __launch_bounds__(Plan<LOGN>::TPS) void block_conv_kernel(
+    BlockArgs a, const float2 *__restrict__ tw) {
+  using PL = Plan<LOGN>;
+  __shared__ float2 lds[PL::kLds];
+  const int t = threadIdx.x;
+  const PairPos q = pair_pos(a, blockIdx.x);
+  float2 v[PL::E];
+  load_pair<PL, BUF>(a, q, t, v);
+  // every input load in flight before the first butterfly consumes one (the
+  // scheduler otherwise splits them into dependent batches)
+  __builtin_amdgcn_sched_barrier(0);
+  fft::transform<PL, false, false>(v, lds, t, tw);
+  mul_spectrum<PL>(a, q, t, v);
   fft::transform<PL, true, true>(v, lds, t, tw);
+  store_pair<PL, BUF>(a, q, t, v);
+}
 
-  constexpr int RI = PL::radix(0);  // last radix of the reversed plan
-  float *y0 = a.y + sig0 * a.ys;
-  float *y1 = a.y + sig1 * a.ys;
-#pragma unroll
-  for (int b = 0; b < PL::E / RI; b++)
-#pragma unroll
-    for (int j = 0; j < RI; j++) {
-      const int n = reg_index<PL, RI>(t, b, j) - a.pre;
-      if (n < 0 || n >= a.step) continue;
-      const float2 r = v[b * RI + j];
-      const long long o0 = static_cast<long long>(b0) * a.step + n;
-      const long long o1 = static_cast<long long>(b1) * a.step + n;
-      if (ok0 && o0 < a.ylen) y0[o0] = r.x * a.scale;
-      if (ok1 && o1 < a.ylen) y1[o1] = r.y * a.scale;
-    }
+// Buffer addressing needs every byte offset of a row in 31 bits.
+inline bool buffer_ok(const BlockArgs &a) {
+  return g_conv_buf && a.xlen < (1 << 29) && a.ylen < (1 << 29);
 }
 
 template <int LOGN>
 void launch_block_t(const BlockArgs &a, const float2 *tw, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>((a.nslots + 1) / 2);
-  hipLaunchKernelGGL((block_conv_kernel<LOGN>), dim3(grid), dim3(Plan<LOGN>::TPS),
-                     0, s, a, tw);
+  if (buffer_ok(a))
+    hipLaunchKernelGGL((block_conv_kernel<LOGN, true>), dim3(grid), dim3(Plan<LOGN>::TPS),
+                       0, s, a, tw);
+  else
+    hipLaunchKernelGGL((block_conv_kernel<LOGN, false>), dim3(grid), dim3(Plan<LOGN>::TPS),
+                       0, s, a, tw);
 }
+
 
 // ------------------------------------------ large FFT path (four-step)
 // z[p][n] = x[2p][n] + i x[2p+1][n] (zero padded to 2^logm)
@@ -318,6 +416,9 @@ __global__ __launch_bounds__(256) void spectrum_mul_kernel(
 // Tuning knob (vs_tune_set("os_block_log_max", n)): cap of the overlap-save
 // block size, for A/B measurements.
 int g_os_log_max = fft::kMaxLdsLog;
+// Tuning knob (vs_tune_set("conv_buffer", 0/1)): buffer-descriptor loads and
+// stores in the fused block kernels.
+int g_conv_buf = 1;
 
 int os_block_log(int hlen) {
   // Reference block size 2^(floor(log2 M) + 2) (src/convolve.c:116-121),
@@ -496,6 +597,10 @@ vs_status vs_tune_set(const char *key, int value) {
   if (std::strcmp(key, "os_block_log_max") == 0) {
     VS_REQUIRE(value >= 4 && value <= fft::kMaxLdsLog, "os_block_log_max out of range");
     conv::g_os_log_max = value;
+    return VS_OK;
+  }
+  if (std::strcmp(key, "conv_buffer") == 0) {
+    conv::g_conv_buf = value != 0;
     return VS_OK;
   }
   set_error("vs_tune_set: unknown key '%s'", key);

@@ -23,6 +23,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace vs {
 namespace fft {
 
@@ -184,6 +186,65 @@ __device__ __forceinline__ void dft(float2 *v) {
 // LDS index with one pad slot per 16 complex elements.
 __device__ __forceinline__ int pad(int e) { return e + (e >> 4); }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a full
+// workgroup fence: every wave drains vmcnt at every LDS exchange, i.e. waits
+// for its prefetches and for the stores of earlier outputs.  The passes only
+// exchange data through LDS.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+constexpr int ilog2c(int r) {
+  int l = 0;
+  while ((1 << l) < r) l++;
+  return l;
+}
+
+// Twiddle sources for Pass::run.  TableTw reads the per-size table at every
+// pass; RegTw holds every twiddle one thread needs for a whole transform in
+// registers, loaded once -- a persistent kernel keeps them across its loop,
+// so its transforms issue no global loads at all.
+struct TableTw {
+  const float2 *__restrict__ tw;
+  template <class PL, bool REV, int Q>
+  __device__ __forceinline__ float2 get(int, int, int idx) const { return tw[idx]; }
+};
+
+template <class PL, bool REV>
+struct RegTw {
+  static constexpr int R(int q) { return REV ? PL::radix_rev(q) : PL::radix(q); }
+  // first slot of pass q (pass 0 has no twiddles)
+  static constexpr int offset(int q) {
+    int o = 0;
+    for (int i = 1; i < q; i++) o += (PL::E / R(i)) * ilog2c(R(i));
+    return o;
+  }
+  static constexpr int kCount = offset(PL::NPASS) > 0 ? offset(PL::NPASS) : 1;
+  float2 w[kCount];
+
+  template <int Q = 1>
+  __device__ __forceinline__ void load(int t, const float2 *__restrict__ tw) {
+    if constexpr (Q < PL::NPASS) {
+      constexpr int RQ = R(Q), P = PL::stride(Q, REV), S = PL::N / (P * RQ);
+      constexpr int LR = ilog2c(RQ);
+#pragma unroll
+      for (int b = 0; b < PL::E / RQ; b++) {
+        const int k = (t + b * PL::TPS) & (P - 1);
+#pragma unroll
+        for (int q = 0; q < LR; q++) w[offset(Q) + b * LR + q] = tw[(1 << q) * k * S];
+      }
+      load<Q + 1>(t, tw);
+    }
+  }
+  template <class PL2, bool REV2, int Q>
+  __device__ __forceinline__ float2 get(int b, int q, int) const {
+    static_assert(REV2 == REV, "twiddle set built for the other radix order");
+    return w[offset(Q) + b * ilog2c(R(Q)) + q];
+  }
+};
+
 // Compile-time pass plan for N = 2^LOGN, 16 points per thread (N >= 16).
 template <int LOGN_>
 struct Plan {
@@ -227,8 +288,8 @@ struct Pass {
   static constexpr int P = PL::stride(Q, REV);
   static constexpr int NB = PL::E / R;
 
-  __device__ static void run(float2 (&v)[PL::E], float2 *lds, int t,
-                             const float2 *__restrict__ tw) {
+  template <class TW>
+  __device__ static void run(float2 (&v)[PL::E], float2 *lds, int t, const TW &tw) {
 #pragma unroll
     for (int b = 0; b < NB; b++) {
       const int i = t + b * PL::TPS;
@@ -240,7 +301,8 @@ struct Pass {
         constexpr int S = PL::N / (P * R);
         float2 wb[R >= 32 ? 5 : 4];
 #pragma unroll
-        for (int q = 0; (1 << q) < R; q++) wb[q] = tw[(1 << q) * k * S];
+        for (int q = 0; (1 << q) < R; q++)
+          wb[q] = tw.template get<PL, REV, Q>(b, q, (1 << q) * k * S);
 #pragma unroll
         for (int j = 1; j < R; j++) {
           float2 w = make_float2(1.f, 0.f);
@@ -265,7 +327,7 @@ struct Pass {
 #pragma unroll
         for (int j = 0; j < R; j++) lds[pad(base + j * P)] = v[b * R + j];
       }
-      __syncthreads();
+      lds_barrier();
       constexpr int R2 = REV ? PL::radix_rev(Q + 1) : PL::radix(Q + 1);
 #pragma unroll
       for (int b = 0; b < PL::E / R2; b++) {
@@ -274,7 +336,7 @@ struct Pass {
         for (int j = 0; j < R2; j++)
           v[b * R2 + j] = lds[pad(i + j * (PL::N / R2))];
       }
-      __syncthreads();
+      lds_barrier();
       Pass<PL, INV, REV, Q + 1>::run(v, lds, t, tw);
     }
   }
@@ -288,11 +350,13 @@ __device__ __forceinline__ int reg_index(int t, int b, int j) {
 }
 
 // Full transform: v (inputs of the first pass, pattern reg_index<first R>)
-// -> v (outputs of the last pass, pattern reg_index<last R>).
-template <class PL, bool INV, bool REV>
-__device__ __forceinline__ void transform(float2 (&v)[PL::E], float2 *lds,
-                                          int t, const float2 *__restrict__ tw) {
-  Pass<PL, INV, REV, 0>::run(v, lds, t, tw);
+// -> v (outputs of the last pass, pattern reg_index<last R>).  `tw` is the
+// twiddle table (const float2 *) or a preloaded RegTw<PL, REV>.
+template <class PL, bool INV, bool REV, class TW>
+__device__ __forceinline__ void transform(float2 (&v)[PL::E], float2 *lds, int t,
+                                          const TW &tw) {
+  if constexpr (std::is_class_v<TW>) Pass<PL, INV, REV, 0>::run(v, lds, t, tw);
+  else Pass<PL, INV, REV, 0>::run(v, lds, t, TableTw{tw});
 }
 
 }  // namespace fft

@@ -1408,14 +1408,15 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
   if (variant < 0) variant = default_variant();
   if (variant < 0) {
     // Largest tile that still gives every CU work (A/B on MI355X,
-    // profiles/r1/sgemm_variants.md): the three-stage LDS-DMA kernels when
-    // the shape is NN and whole tiles (256x256 from 256 tiles, else 128x128),
+    // profiles/r1/sgemm_variants.md, sgemm_gen5_ab_v2.log): the LDS-DMA
+    // kernels when the shape is NN and whole tiles (gen 5 256x256 from 256
+    // tiles, else gen 5 128x128),
     // otherwise 256x128 (gen 1) / 128x128 (gen 2) / 64x64 register-staged.
     const long t128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
     const long t256sq = static_cast<long>((m + 255) / 256) * ((n + 255) / 256) * batch;
-    if (t256sq >= 256) variant = 15;       // falls back to 3 unless NN whole tiles
-    else if (t128 >= 256) variant = 16;    // falls back to 5
+    if (t256sq >= 256) variant = 22;       // gen 5 256x256; falls back to 3 unless NN whole tiles
+    else if (t128 >= 256) variant = 21;    // gen 5 128x128; falls back to 5
     else if (t256 >= 512) variant = 3;
     else variant = 0;
   }

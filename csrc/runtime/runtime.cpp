@@ -128,6 +128,23 @@ unsigned elementwise_grid(size_t work_items, unsigned block) {
   return static_cast<unsigned>(g);
 }
 
+int device_cu_count() {
+  static int cache[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0) {
+      (void)hipGetLastError();
+      n = 256;
+    }
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 static bool sync_stage() {
   static const bool v = env_int("VELES_SYNC_STAGE", 0) != 0;
   return v;

@@ -85,6 +85,9 @@ bool is_device_pointer(const void *p);
 size_t gpu_min_elems();
 // Launch helper: grid size for a grid-stride elementwise kernel.
 unsigned elementwise_grid(size_t work_items, unsigned block);
+// Compute units of the current device (cached; 256 on MI355X), for sizing
+// persistent grids.
+int device_cu_count();
 
 // ------------------------------------------------------- scratch memory
 // Device scratch from the library's caching pool (stream-tagged blocks, see

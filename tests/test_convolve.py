@@ -150,3 +150,27 @@ def test_rfft_irfft(n):
     assert np.abs(got - ref).max() <= 1e-5 * np.sqrt(n) * np.log2(n) + 1e-5
     back = ops.irfft(X.float().cuda(), n).cpu().double() / n
     np.testing.assert_allclose(back.numpy(), x.double().numpy(), atol=3e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knobs", [{}, {"conv_buffer": 0}])
+@pytest.mark.parametrize("hlen", [300, 4096])
+def test_device_conv1d_many_blocks(knobs, hlen):
+    """Overlap-save with more block pairs than CUs and a ragged last block,
+    buffer-descriptor and flat addressing; float64 FFT reference."""
+    import torch
+    from veles.simd_amd import _lib, ops
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(hlen)
+    x = torch.randn(24, 300001, generator=g)
+    h = torch.randn(hlen, generator=g)
+    try:
+        for k, v in knobs.items():
+            _lib.check(lib.vs_tune_set(k.encode(), v), k)
+        y = ops.conv1d(x.cuda(), h.cuda(), algorithm=3).cpu().double().numpy()
+    finally:
+        _lib.check(lib.vs_tune_set(b"conv_buffer", 1))
+    n = x.shape[1] + hlen - 1
+    m = 1 << (n - 1).bit_length()
+    ref = np.fft.irfft(np.fft.rfft(x.double().numpy(), m) * np.fft.rfft(h.double().numpy(), m), m)[:, :n]
+    assert np.abs(y - ref).max() <= 1e-5 * np.abs(ref).max()

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Conv1d throughput sweep (Msamples/s of input) over algorithms, filter
-lengths and overlap-save block caps, interleaved in one process."""
+lengths and overlap-save block caps, interleaved in one process.
+KNOBS="name=v0/v1,..." adds A/B arms of vs_tune_set knobs on the auto path
+(e.g. KNOBS="conv_buffer=0/1"); every arm is checked against
+the first one."""
 import ctypes
 import json
 import os
@@ -14,6 +17,7 @@ from veles.simd_amd import _lib  # noqa: E402
 
 lib = _lib.lib()
 lib.vs_tune_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
+DEFAULTS = {"conv_buffer": 1}
 
 
 def main():
@@ -28,16 +32,31 @@ def main():
         h = torch.randn(hlen, device="cuda")
         ylen = xlen + hlen - 1
         y = torch.empty(batch, ylen, device="cuda")
-        variants = [("auto", 0, 14), ("direct", 1, 14), ("fft", 2, 14)]
-        variants += [(f"os{lg}", 3, lg) for lg in (11, 12, 13, 14) if (1 << lg) > 2 * hlen + 64]
+        knobs = [kv.split("=") for kv in os.environ.get("KNOBS", "").split(",") if kv]
+        variants = [("auto", 0, 14, {})]
+        for name, vals in knobs:
+            variants += [(f"{name}={v}", 0, 14, {name: int(v)}) for v in vals.split("/")]
+        if not knobs:
+            variants += [("direct", 1, 14, {}), ("fft", 2, 14, {})]
+            variants += [(f"os{lg}", 3, lg, {}) for lg in (11, 12, 13, 14)
+                         if (1 << lg) > 2 * hlen + 64]
         times = {v[0]: [] for v in variants}
         ev0, ev1 = torch.cuda.Event(True), torch.cuda.Event(True)
+        ref = None
         for r in range(rounds):
-            for name, algo, lg in variants:
+            for name, algo, lg, kn in variants:
                 lib.vs_tune_set(b"os_block_log_max", lg)
+                for k, v in kn.items():
+                    lib.vs_tune_set(k.encode(), v)
                 run = lambda: lib.vs_conv1d(algo, 0, x.data_ptr(), xlen, xlen, h.data_ptr(),
                                             hlen, 0, y.data_ptr(), ylen, batch, s)
                 assert run() == 0, lib.vs_last_error()
+                if r == 0:
+                    if ref is None:
+                        ref = y.clone()
+                    else:
+                        err = (y - ref).abs().max().item() / ref.abs().max().item()
+                        assert err < 1e-4, (name, err)
                 reps = 3
                 ev0.record()
                 for _ in range(reps):
@@ -45,6 +64,8 @@ def main():
                 ev1.record()
                 torch.cuda.synchronize()
                 times[name].append(ev0.elapsed_time(ev1) / reps)
+                for k in kn:  # back to the library defaults
+                    lib.vs_tune_set(k.encode(), DEFAULTS.get(k, 1))
         lib.vs_tune_set(b"os_block_log_max", 14)
         out = {k: round(xlen * batch / statistics.median(v) / 1e3, 1) for k, v in times.items()}
         res[hlen] = out
