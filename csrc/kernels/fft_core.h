@@ -288,8 +288,12 @@ struct Pass {
   static constexpr int P = PL::stride(Q, REV);
   static constexpr int NB = PL::E / R;
 
-  template <class TW>
-  __device__ static void run(float2 (&v)[PL::E], float2 *lds, int t, const TW &tw) {
+  // LT = float2: one exchange of the complex values through an N-point LDS
+  // image.  LT = float ("split"): the real parts, then the imaginary parts,
+  // through an N-float image -- half the LDS (two 16384-point workgroups per
+  // CU instead of one) for twice the barriers.
+  template <class TW, class LT>
+  __device__ static void run(float2 (&v)[PL::E], LT *lds, int t, const TW &tw) {
 #pragma unroll
     for (int b = 0; b < NB; b++) {
       const int i = t + b * PL::TPS;
@@ -319,24 +323,45 @@ struct Pass {
       dft<R, INV>(&v[b * R]);
     }
     if constexpr (Q + 1 < PL::NPASS) {
-#pragma unroll
-      for (int b = 0; b < NB; b++) {
-        const int i = t + b * PL::TPS;
-        const int k = i & (P - 1);
-        const int base = (i - k) * R + k;
-#pragma unroll
-        for (int j = 0; j < R; j++) lds[pad(base + j * P)] = v[b * R + j];
-      }
-      lds_barrier();
       constexpr int R2 = REV ? PL::radix_rev(Q + 1) : PL::radix(Q + 1);
+      // this pass's outputs (one component via `comp`) -> LDS
+      const auto put = [&](auto comp) {
 #pragma unroll
-      for (int b = 0; b < PL::E / R2; b++) {
-        const int i = t + b * PL::TPS;
+        for (int b = 0; b < NB; b++) {
+          const int i = t + b * PL::TPS;
+          const int k = i & (P - 1);
+          const int base = (i - k) * R + k;
 #pragma unroll
-        for (int j = 0; j < R2; j++)
-          v[b * R2 + j] = lds[pad(i + j * (PL::N / R2))];
+          for (int j = 0; j < R; j++) lds[pad(base + j * P)] = comp(v[b * R + j]);
+        }
+      };
+      // LDS -> the next pass's inputs, element e of v via `sink(e, value)`
+      const auto get = [&](auto sink) {
+#pragma unroll
+        for (int b = 0; b < PL::E / R2; b++) {
+          const int i = t + b * PL::TPS;
+#pragma unroll
+          for (int j = 0; j < R2; j++) sink(b * R2 + j, lds[pad(i + j * (PL::N / R2))]);
+        }
+      };
+      if constexpr (std::is_same_v<LT, float2>) {
+        put([](float2 z) { return z; });
+        lds_barrier();
+        get([&](int e, float2 z) { v[e] = z; });
+        lds_barrier();
+      } else {
+        // Once every real part is in LDS the registers' real halves are
+        // dead, so the new real parts land in them in place while the
+        // imaginary halves still hold the old ones: no temporary array.
+        put([](float2 z) { return z.x; });
+        lds_barrier();
+        get([&](int e, float z) { v[e].x = z; });
+        lds_barrier();
+        put([](float2 z) { return z.y; });
+        lds_barrier();
+        get([&](int e, float z) { v[e].y = z; });
+        lds_barrier();
       }
-      lds_barrier();
       Pass<PL, INV, REV, Q + 1>::run(v, lds, t, tw);
     }
   }
@@ -352,8 +377,8 @@ __device__ __forceinline__ int reg_index(int t, int b, int j) {
 // Full transform: v (inputs of the first pass, pattern reg_index<first R>)
 // -> v (outputs of the last pass, pattern reg_index<last R>).  `tw` is the
 // twiddle table (const float2 *) or a preloaded RegTw<PL, REV>.
-template <class PL, bool INV, bool REV, class TW>
-__device__ __forceinline__ void transform(float2 (&v)[PL::E], float2 *lds, int t,
+template <class PL, bool INV, bool REV, class TW, class LT>
+__device__ __forceinline__ void transform(float2 (&v)[PL::E], LT *lds, int t,
                                           const TW &tw) {
   if constexpr (std::is_class_v<TW>) Pass<PL, INV, REV, 0>::run(v, lds, t, tw);
   else Pass<PL, INV, REV, 0>::run(v, lds, t, TableTw{tw});
