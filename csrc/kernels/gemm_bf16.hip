@@ -53,53 +53,96 @@ __device__ __forceinline__ float bf16_float(uint16_t b) {
 // dst[r][c] (r < rows_p, c < cols_p, row stride cols_p) from the logical
 // operand element (r, c) = src[r * ld + c] (TRANS = 0) or src[c * ld + r]
 // (TRANS = 1), zero outside rows x cols.  SPLIT: fp32 source, writes hi and
-// lo images; else bf16 source (uint16 bits), one image.  32x32 tiles through
-// LDS so both the global read and the write are coalesced when transposing.
+// lo images; else bf16 source (uint16 bits), one image.  64 x 64 tiles, one
+// 8-element chunk per thread and step: 16-byte loads along the source's
+// contiguous dimension (VEC: ld, the batch stride and the base are 8-element
+// aligned) and 16-byte stores along c; TRANS turns the tile round through a
+// [64][65] float LDS image (conflict-free both ways).  Rows of the source
+// that end inside a chunk fall back to guarded scalar loads.
+template <bool SPLIT>
+__device__ __forceinline__ void load8(const void *src, int64_t off, bool vec, int lim,
+                                      int64_t step, float (&v)[8]) {
+  if (vec && lim >= 8) {
+    if (SPLIT) {
+      const float4 *p = reinterpret_cast<const float4 *>(static_cast<const float *>(src) + off);
+      const float4 x = p[0], y = p[1];
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+      v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    } else {
+      const uint4 x = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(src) + off);
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        v[2 * j] = __uint_as_float(w[j] << 16);
+        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int64_t o = off + j * step;
+    v[j] = j < lim ? (SPLIT ? static_cast<const float *>(src)[o]
+                            : bf16_float(static_cast<const uint16_t *>(src)[o]))
+                   : 0.f;
+  }
+}
+
+template <bool SPLIT>
+__device__ __forceinline__ void store8(uint16_t *hi, uint16_t *lo, int64_t o, const float (&v)[8]) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint16_t h0 = bf16_bits(v[2 * j]), h1 = bf16_bits(v[2 * j + 1]);
+    h[j] = h0 | (static_cast<uint32_t>(h1) << 16);
+    if (SPLIT)
+      l[j] = bf16_bits(v[2 * j] - bf16_float(h0)) |
+             (static_cast<uint32_t>(bf16_bits(v[2 * j + 1] - bf16_float(h1))) << 16);
+  }
+  *reinterpret_cast<uint4 *>(hi + o) = make_uint4(h[0], h[1], h[2], h[3]);
+  if (SPLIT) *reinterpret_cast<uint4 *>(lo + o) = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
 template <bool SPLIT, bool TRANS>
 __global__ __launch_bounds__(256) void pack_kernel(const void *__restrict__ src,
                                                    int64_t ld, int rows, int cols,
                                                    int rows_p, int cols_p,
                                                    uint16_t *__restrict__ hi,
                                                    uint16_t *__restrict__ lo,
-                                                   int64_t sstride, int64_t dstride) {
-  __shared__ float tile[32][33];
-  const int tr = threadIdx.x >> 5, tc = threadIdx.x & 31;  // 8 x 32
-  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
-  const float *sf = static_cast<const float *>(src) + blockIdx.z * sstride;
-  const uint16_t *sh = static_cast<const uint16_t *>(src) + blockIdx.z * sstride;
-  auto fetch = [&](int r, int c) -> float {
-    if (r >= rows || c >= cols) return 0.f;
-    const int64_t off = TRANS ? static_cast<int64_t>(c) * ld + r
-                              : static_cast<int64_t>(r) * ld + c;
-    return SPLIT ? sf[off] : bf16_float(sh[off]);
-  };
+                                                   int64_t sstride, int64_t dstride, bool vec) {
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int sub = threadIdx.x >> 3, ch = (threadIdx.x & 7) * 8;  // 32 x 8 chunks
+  const int64_t sb = blockIdx.z * sstride, db = blockIdx.z * dstride;
   if (TRANS) {
-    // read along r (contiguous in memory), write transposed through LDS
+    __shared__ float tile[64][65];  // [c][r]
 #pragma unroll
-    for (int i = 0; i < 32; i += 8) tile[tc][tr + i] = fetch(r0 + tc, c0 + tr + i);
+    for (int i = 0; i < 2; i++) {
+      const int c = c0 + sub + 32 * i, r = r0 + ch;  // 8 consecutive r of source row c
+      float v[8];
+      load8<SPLIT>(src, sb + static_cast<int64_t>(c) * ld + r, vec,
+                   c < cols ? rows - r : 0, 1, v);
+#pragma unroll
+      for (int j = 0; j < 8; j++) tile[sub + 32 * i][ch + j] = v[j];
+    }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 32; i += 8) {
-      const int r = r0 + tr + i, c = c0 + tc;
-      const float v = tile[tr + i][tc];
-      if (r < rows_p && c < cols_p) {
-        const int64_t o = blockIdx.z * dstride + static_cast<int64_t>(r) * cols_p + c;
-        const uint16_t h = bf16_bits(v);
-        hi[o] = h;
-        if (SPLIT) lo[o] = bf16_bits(v - bf16_float(h));
-      }
+    for (int i = 0; i < 2; i++) {
+      const int r = r0 + sub + 32 * i, c = c0 + ch;
+      if (r >= rows_p || c >= cols_p) continue;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = tile[ch + j][sub + 32 * i];
+      store8<SPLIT>(hi, lo, db + static_cast<int64_t>(r) * cols_p + c, v);
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 32; i += 8) {
-      const int r = r0 + tr + i, c = c0 + tc;
-      if (r < rows_p && c < cols_p) {
-        const float v = fetch(r, c);
-        const int64_t o = blockIdx.z * dstride + static_cast<int64_t>(r) * cols_p + c;
-        const uint16_t h = bf16_bits(v);
-        hi[o] = h;
-        if (SPLIT) lo[o] = bf16_bits(v - bf16_float(h));
-      }
+    for (int i = 0; i < 2; i++) {
+      const int r = r0 + sub + 32 * i, c = c0 + ch;
+      if (r >= rows_p || c >= cols_p) continue;
+      float v[8];
+      load8<SPLIT>(src, sb + static_cast<int64_t>(r) * ld + c, vec,
+                   r < rows ? cols - c : 0, 1, v);
+      store8<SPLIT>(hi, lo, db + static_cast<int64_t>(r) * cols_p + c, v);
     }
   }
 }
@@ -109,7 +152,8 @@ struct Args {
   const uint16_t *a[2];  // [Mp][Kp] images: hi (and lo)
   const uint16_t *b[2];  // [Np][Kp]
   int64_t sa, sb;        // batch strides of the images (elements)
-  int kp;
+  int64_t lda, ldb;      // row strides of the images (elements; >= kp)
+  int kp;                // K extent (a multiple of the k tile)
   int m, n;              // logical output size
   float alpha, beta;
   float *c;
@@ -134,13 +178,13 @@ struct Cfg {
 
 template <int ROWS, int THREADS, int LOADS>
 struct Stage {
-  __device__ static void load(const uint16_t *__restrict__ img, int64_t kp, int row0,
+  __device__ static void load(const uint16_t *__restrict__ img, int64_t ld, int row0,
                               int k0, uint4 (&r)[LOADS]) {
 #pragma unroll
     for (int l = 0; l < LOADS; l++) {
       const int idx = threadIdx.x + l * THREADS;
       const int row = idx / (kBK / 8), kc = (idx % (kBK / 8)) * 8;
-      r[l] = *reinterpret_cast<const uint4 *>(img + (row0 + row) * kp + k0 + kc);
+      r[l] = *reinterpret_cast<const uint4 *>(img + (row0 + row) * ld + k0 + kc);
     }
   }
   __device__ static void store(uint16_t *__restrict__ s, const uint4 (&r)[LOADS]) {
@@ -170,7 +214,6 @@ __global__ __launch_bounds__(C::kThreads) void gemm_kernel(Args g) {
   unsigned tm, tn;
   dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
   const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
-  const int64_t kp = g.kp;
 
   const uint16_t *A[2], *B[2];
 #pragma unroll
@@ -202,8 +245,8 @@ __global__ __launch_bounds__(C::kThreads) void gemm_kernel(Args g) {
   const int nk = g.kp / kBK;
 #pragma unroll
   for (int i = 0; i < NI; i++) {
-    SA::load(A[i], kp, m0, 0, ra[i]);
-    SB::load(B[i], kp, n0, 0, rb[i]);
+    SA::load(A[i], g.lda, m0, 0, ra[i]);
+    SB::load(B[i], g.ldb, n0, 0, rb[i]);
   }
 #pragma unroll
   for (int i = 0; i < NI; i++) {
@@ -218,8 +261,8 @@ __global__ __launch_bounds__(C::kThreads) void gemm_kernel(Args g) {
     if (more) {
 #pragma unroll
       for (int i = 0; i < NI; i++) {
-        SA::load(A[i], kp, m0, (kt + 1) * kBK, ra[i]);
-        SB::load(B[i], kp, n0, (kt + 1) * kBK, rb[i]);
+        SA::load(A[i], g.lda, m0, (kt + 1) * kBK, ra[i]);
+        SB::load(B[i], g.ldb, n0, (kt + 1) * kBK, rb[i]);
       }
     }
 #pragma unroll
@@ -296,21 +339,25 @@ vs_status launch(const Args &g, int batch, hipStream_t s) {
 vs_status pack(bool split, bool trans, const void *src, int64_t ld, int rows, int cols,
                int rows_p, int cols_p, uint16_t *hi, uint16_t *lo, int64_t sstride,
                int batch, hipStream_t s) {
-  const dim3 grid(static_cast<unsigned>((cols_p + 31) / 32),
-                  static_cast<unsigned>((rows_p + 31) / 32), static_cast<unsigned>(batch));
+  // rows_p, cols_p are multiples of the tile sizes (>= 32), so every 8-chunk
+  // of the destination is either wholly inside or wholly outside
+  const dim3 grid(static_cast<unsigned>((cols_p + 63) / 64),
+                  static_cast<unsigned>((rows_p + 63) / 64), static_cast<unsigned>(batch));
   const int64_t dstride = static_cast<int64_t>(rows_p) * cols_p;
+  const bool vec = ld % 8 == 0 && (batch == 1 || sstride % 8 == 0) &&
+                   reinterpret_cast<uintptr_t>(src) % 16 == 0;
   if (split && trans)
     hipLaunchKernelGGL((pack_kernel<true, true>), grid, dim3(256), 0, s, src, ld, rows, cols,
-                       rows_p, cols_p, hi, lo, sstride, dstride);
+                       rows_p, cols_p, hi, lo, sstride, dstride, vec);
   else if (split)
     hipLaunchKernelGGL((pack_kernel<true, false>), grid, dim3(256), 0, s, src, ld, rows, cols,
-                       rows_p, cols_p, hi, lo, sstride, dstride);
+                       rows_p, cols_p, hi, lo, sstride, dstride, vec);
   else if (trans)
     hipLaunchKernelGGL((pack_kernel<false, true>), grid, dim3(256), 0, s, src, ld, rows, cols,
-                       rows_p, cols_p, hi, lo, sstride, dstride);
+                       rows_p, cols_p, hi, lo, sstride, dstride, vec);
   else
     hipLaunchKernelGGL((pack_kernel<false, false>), grid, dim3(256), 0, s, src, ld, rows,
-                       cols, rows_p, cols_p, hi, lo, sstride, dstride);
+                       cols, rows_p, cols_p, hi, lo, sstride, dstride, vec);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
@@ -355,7 +402,7 @@ __device__ __forceinline__ int swz(int row, int c) {
 
 // DMA one image tile (ROWS x BK at row0, k0) into the LDS image at `dst`.
 template <class C, int INSTR>
-__device__ __forceinline__ void dma_image(const uint16_t *__restrict__ img, int64_t kp,
+__device__ __forceinline__ void dma_image(const uint16_t *__restrict__ img, int64_t ld,
                                           int row0, int k0, uint8_t *dst, int wave,
                                           int lane) {
 #pragma unroll
@@ -364,7 +411,7 @@ __device__ __forceinline__ void dma_image(const uint16_t *__restrict__ img, int6
     const int row = j * C::RPI + lane / C::NC;  // tile row this lane fills
     const int pc = lane % C::NC;                // physical chunk it fills
     const int c = swz<C>(row, pc);              // logical chunk stored there
-    const uint16_t *src = img + static_cast<int64_t>(row0 + row) * kp + k0 + 8 * c;
+    const uint16_t *src = img + static_cast<int64_t>(row0 + row) * ld + k0 + 8 * c;
     __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(dst + j * 1024), 16, 0,
                                      0);
   }
@@ -385,7 +432,6 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
   unsigned tm, tn;
   dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
   const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
-  const int64_t kp = g.kp;
   const uint16_t *A[2], *B[2];
 #pragma unroll
   for (int i = 0; i < NI; i++) {
@@ -406,8 +452,8 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
   auto stage = [&](int buf, int k0) {
 #pragma unroll
     for (int i = 0; i < NI; i++) {
-      dma_image<C, C::kInstrA>(A[i], kp, m0, k0, img_a(buf, i), wid, lane);
-      dma_image<C, C::kInstrB>(B[i], kp, n0, k0, img_b(buf, i), wid, lane);
+      dma_image<C, C::kInstrA>(A[i], g.lda, m0, k0, img_a(buf, i), wid, lane);
+      dma_image<C, C::kInstrB>(B[i], g.ldb, n0, k0, img_b(buf, i), wid, lane);
     }
   };
 
@@ -511,7 +557,6 @@ __global__ __launch_bounds__(C::kThreads) void gemm_ring_kernel(Args g) {
   unsigned tm, tn;
   dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
   const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
-  const int64_t kp = g.kp;
   const uint16_t *A[2], *B[2];
 #pragma unroll
   for (int i = 0; i < NI; i++) {
@@ -528,9 +573,9 @@ __global__ __launch_bounds__(C::kThreads) void gemm_ring_kernel(Args g) {
   auto stage = [&](uint8_t *base, int k0) {
 #pragma unroll
     for (int i = 0; i < NI; i++) {
-      dma_image<C, C::kInstrA>(A[i], kp, m0, k0, base + i * C::kImgA, wid, lane);
-      dma_image<C, C::kInstrB>(B[i], kp, n0, k0, base + NI * C::kImgA + i * C::kImgB, wid,
-                               lane);
+      dma_image<C, C::kInstrA>(A[i], g.lda, m0, k0, base + i * C::kImgA, wid, lane);
+      dma_image<C, C::kInstrB>(B[i], g.ldb, n0, k0, base + NI * C::kImgA + i * C::kImgB,
+                               wid, lane);
     }
   };
   floatx16 acc[TM][TN];
@@ -681,24 +726,53 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   const int mp = (m + bm - 1) / bm * bm, np = (n + bn - 1) / bn * bn;
   const int kp = k == 0 ? bk : (k + bk - 1) / bk * bk;
   const int ni = split ? 2 : 1;
+  // A bf16 operand already stored K-contiguous ([rows][ld]: A unless ta, B
+  // when tb) with whole tiles and aligned rows is read in place -- no
+  // prepass, no workspace (VELES_GEMM_BF16_PACK=1 forces the copy).
+  static const bool force_pack = [] {
+    const char *e = std::getenv("VELES_GEMM_BF16_PACK");
+    return e && *e == '1';
+  }();
+  const auto direct = [&](bool kcontig, int rows, int rows_p, const void *p, int64_t ld,
+                          int64_t st) {
+    return !split && !force_pack && kcontig && rows == rows_p && k == kp && ld % 8 == 0 &&
+           (batch == 1 || st % 8 == 0) && reinterpret_cast<uintptr_t>(p) % 16 == 0;
+  };
+  const bool da = direct(ta == 0, m, mp, a, lda, sa);
+  const bool db = direct(tb != 0, n, np, b, ldb, sb);
   const size_t ea = static_cast<size_t>(mp) * kp, eb = static_cast<size_t>(np) * kp;
+  const size_t wa = da ? 0 : ea * ni * batch, wb = db ? 0 : eb * ni * batch;
   DeviceBuffer buf;
-  VS_TRY(buf.alloc((ea + eb) * ni * batch * sizeof(uint16_t), s));
-  uint16_t *pa = buf.as<uint16_t>();
-  uint16_t *pb = pa + ea * ni * batch;
-  // A: logical (M x K), element (r, c) at a[r*lda + c] unless ta.
-  VS_TRY(pack(split, ta != 0, a, lda, m, k, mp, kp, pa, split ? pa + ea * batch : nullptr, sa,
-              batch, s));
-  // B: logical op(B)^T (N x K): element (n, k) at b[k*ldb + n] unless tb.
-  VS_TRY(pack(split, tb == 0, b, ldb, n, k, np, kp, pb, split ? pb + eb * batch : nullptr, sb,
-              batch, s));
+  if (wa + wb) VS_TRY(buf.alloc((wa + wb) * sizeof(uint16_t), s));
+  uint16_t *pa = da ? nullptr : buf.as<uint16_t>();
+  uint16_t *pb = db ? nullptr : buf.as<uint16_t>() + wa;
   Args g{};
-  g.a[0] = pa;
-  g.a[1] = split ? pa + ea * batch : nullptr;
-  g.b[0] = pb;
-  g.b[1] = split ? pb + eb * batch : nullptr;
-  g.sa = static_cast<int64_t>(ea);
-  g.sb = static_cast<int64_t>(eb);
+  // A: logical (M x K), element (r, c) at a[r*lda + c] unless ta.
+  if (da) {
+    g.a[0] = static_cast<const uint16_t *>(a);
+    g.sa = batch == 1 ? 0 : sa;
+    g.lda = lda;
+  } else {
+    VS_TRY(pack(split, ta != 0, a, lda, m, k, mp, kp, pa, split ? pa + ea * batch : nullptr,
+                sa, batch, s));
+    g.a[0] = pa;
+    g.a[1] = split ? pa + ea * batch : nullptr;
+    g.sa = static_cast<int64_t>(ea);
+    g.lda = kp;
+  }
+  // B: logical op(B)^T (N x K): element (n, k) at b[k*ldb + n] unless tb.
+  if (db) {
+    g.b[0] = static_cast<const uint16_t *>(b);
+    g.sb = batch == 1 ? 0 : sb;
+    g.ldb = ldb;
+  } else {
+    VS_TRY(pack(split, tb == 0, b, ldb, n, k, np, kp, pb, split ? pb + eb * batch : nullptr,
+                sb, batch, s));
+    g.b[0] = pb;
+    g.b[1] = split ? pb + eb * batch : nullptr;
+    g.sb = static_cast<int64_t>(eb);
+    g.ldb = kp;
+  }
   g.kp = kp;
   g.m = m;
   g.n = n;

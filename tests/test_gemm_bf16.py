@@ -135,3 +135,46 @@ def test_every_kernel_variant(variant):
                                             c.data_ptr(), n, s), "bf16")
         ref1 = (ah.double().T if ta else ah.double()) @ (bh.double().T if tb else bh.double())
         assert (c.double() - ref1).abs().max().item() <= 2e-6 * k + 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("ld_pad", [0, 8, 4])
+def test_whole_tile_operands_read_in_place(variant, ld_pad):
+    """bf16 operands stored K-contiguous with whole tiles skip the pack
+    prepass and are read in place with their own row stride (ld_pad 0 / 8);
+    a stride that is not 8-aligned (ld_pad 4) takes the packed path with
+    scalar loads.  All four transpose combinations, so A and B each go
+    in place and packed."""
+    import ctypes
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    m, n, k = 512, 512, 256
+    g = torch.Generator(device="cuda").manual_seed(100 + variant)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for ta, tb in ((0, 0), (0, 1), (1, 0), (1, 1)):
+        ra, ca = (k, m) if ta else (m, k)
+        rb, cb = (n, k) if tb else (k, n)
+        af = (torch.rand(ra, ca + ld_pad, device="cuda", generator=g) * 2 - 1).bfloat16()
+        bf = (torch.rand(rb, cb + ld_pad, device="cuda", generator=g) * 2 - 1).bfloat16()
+        a, b = af[:, :ca], bf[:, :cb]
+        c = torch.full((m, n), float("nan"), device="cuda")
+        _lib.check(lib.vs_gemm_bf16_variant(variant, ta, tb, m, n, k, 1.0, a.data_ptr(),
+                                            af.shape[1], b.data_ptr(), bf.shape[1], 0.0,
+                                            c.data_ptr(), n, s), "bf16")
+        ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
+        assert (c.double() - ref).abs().max().item() <= 2e-6 * k + 1e-6, (ta, tb)
+
+
+@pytest.mark.gpu
+def test_batched_in_place_operands():
+    """Strided-batched bf16 with every operand read in place (A batch
+    stride, B shared with stride 0) and with B transposed per batch."""
+    g = torch.Generator(device="cuda").manual_seed(21)
+    a = (torch.rand(3, 256, 128, device="cuda", generator=g) - 0.5).bfloat16()
+    b = (torch.rand(128, 256, device="cuda", generator=g) - 0.5).bfloat16()
+    assert (ops.gemm_bf16(a, b).double() - a.double() @ b.double()).abs().max().item() < 1e-4
+    bt = (torch.rand(3, 256, 128, device="cuda", generator=g) - 0.5).bfloat16()
+    c = ops.gemm_bf16(a, bt, False, True)
+    ref = a.double() @ bt.double().transpose(1, 2)
+    assert (c.double() - ref).abs().max().item() < 1e-4
