@@ -544,11 +544,17 @@ __device__ __forceinline__ void bf_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 0xF) | ((N >> 4) << 14));
 }
 
-template <class C>
+// NS = 4 (BK = 32 images, 4 x 32 KiB): two tiles' DMA stay in flight
+// across each barrier instead of one -- more bytes in flight per CU against
+// the L2 / HBM latency, which the PMC wait fraction of the two-stage kernel
+// (39 % of wave cycles waiting, no LDS bank conflicts) points at.
+template <class C, int NS>
 __global__ __launch_bounds__(C::kThreads) void gemm_ring_kernel(Args g) {
+  static_assert(NS == 3 || NS == 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) uint8_t r0[C::kStage];
   __shared__ __attribute__((aligned(1024))) uint8_t r1[C::kStage];
   __shared__ __attribute__((aligned(1024))) uint8_t r2[C::kStage];
+  __shared__ __attribute__((aligned(1024))) uint8_t r3[NS == 4 ? C::kStage : 1];
   constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
   constexpr int kInstr = NI * (C::kInstrA + C::kInstrB);  // DMA per wave per tile
   const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
@@ -619,19 +625,32 @@ __global__ __launch_bounds__(C::kThreads) void gemm_ring_kernel(Args g) {
   const int nk = g.kp / C::BK;
   stage(r0, 0);
   if (nk > 1) stage(r1, C::BK);
-#define VS_RING_STEP(CUR, NEXT2)                             \
+  if (NS == 4 && nk > 2) stage(r2, 2 * C::BK);
+  // tile kt's DMA has landed once at most the later tiles' DMA (kt+1 ..
+  // kt+NS-2, those that exist) are outstanding
+#define VS_RING_STEP(CUR, NEXT)                              \
   if (kt < nk) {                                             \
-    if (kt + 1 < nk) bf_wait_vmcnt<kInstr>();                \
+    if (NS == 4 && kt + 2 < nk) bf_wait_vmcnt<2 * kInstr>(); \
+    else if (kt + 1 < nk) bf_wait_vmcnt<kInstr>();           \
     else bf_wait_vmcnt<0>();                                 \
     __builtin_amdgcn_s_barrier();                            \
-    if (kt + 2 < nk) stage(NEXT2, (kt + 2) * C::BK);         \
+    if (kt + NS - 1 < nk) stage(NEXT, (kt + NS - 1) * C::BK); \
     compute(CUR);                                            \
   }                                                          \
   kt++;
-  for (int kt = 0; kt < nk;) {
-    VS_RING_STEP(r0, r2)
-    VS_RING_STEP(r1, r0)
-    VS_RING_STEP(r2, r1)
+  if constexpr (NS == 3) {
+    for (int kt = 0; kt < nk;) {
+      VS_RING_STEP(r0, r2)
+      VS_RING_STEP(r1, r0)
+      VS_RING_STEP(r2, r1)
+    }
+  } else {
+    for (int kt = 0; kt < nk;) {
+      VS_RING_STEP(r0, r3)
+      VS_RING_STEP(r1, r0)
+      VS_RING_STEP(r2, r1)
+      VS_RING_STEP(r3, r2)
+    }
   }
 #undef VS_RING_STEP
 
@@ -655,11 +674,11 @@ __global__ __launch_bounds__(C::kThreads) void gemm_ring_kernel(Args g) {
     }
 }
 
-template <class C>
+template <class C, int NS = 3>
 vs_status launch_ring(const Args &g, int batch, hipStream_t s) {
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
-  hipLaunchKernelGGL(gemm_ring_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
+  hipLaunchKernelGGL((gemm_ring_kernel<C, NS>), dim3(tiles, 1, static_cast<unsigned>(batch)),
                      dim3(C::kThreads), 0, s, g);
   VS_HIP(hipGetLastError());
   return VS_OK;
@@ -708,17 +727,17 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
     variant = t256 >= 256 ? 2 : (t256 >= 128 ? 1 : 0);
   }
-  VS_REQUIRE(variant >= 0 && variant <= 4, "gemm_bf16: unknown variant %d", variant);
+  VS_REQUIRE(variant >= 0 && variant <= 5, "gemm_bf16: unknown variant %d", variant);
   int bm = variant == 1 ? 256 : 128, bn = 128, bk = kBK;
   if (variant == 2) {
     bm = split ? G3::BM : G1::BM;
     bn = split ? G3::BN : G1::BN;
     bk = split ? G3::BK : G1::BK;
-  } else if (variant == 3 || (variant == 4 && split)) {
+  } else if (variant == 3 || (variant >= 4 && split)) {
     bm = split ? R3::BM : R1::BM;
     bn = split ? R3::BN : R1::BN;
     bk = split ? R3::BK : R1::BK;
-  } else if (variant == 4) {
+  } else if (variant >= 4) {
     bm = R1S::BM;
     bn = R1S::BN;
     bk = R1S::BK;
@@ -782,9 +801,10 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   g.ldc = ldc;
   g.sc = sc;
   if (variant == 2) return split ? launch_glds<G3>(g, batch, s) : launch_glds<G1>(g, batch, s);
-  if (variant == 3 || (variant == 4 && split))
+  if (variant == 3 || (variant >= 4 && split))
     return split ? launch_ring<R3>(g, batch, s) : launch_ring<R1>(g, batch, s);
   if (variant == 4) return launch_ring<R1S>(g, batch, s);
+  if (variant == 5) return launch_ring<R1S, 4>(g, batch, s);
   if (split) return variant == 1 ? launch<C3L>(g, batch, s) : launch<C3>(g, batch, s);
   return variant == 1 ? launch<C1L>(g, batch, s) : launch<C1>(g, batch, s);
 }

@@ -45,6 +45,14 @@ def main():
                                                         bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
             "bf16_v4": lambda: lib.vs_gemm_bf16_variant(4, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
                                                         bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
+            "bf16_v5": lambda: lib.vs_gemm_bf16_variant(5, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
+                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
+            "bf16_nt_v2": lambda: lib.vs_gemm_bf16_variant(2, 0, 1, n, n, n, 1.0, ah.data_ptr(), n,
+                                                           bh.data_ptr(), n, 0.0, c.data_ptr(), n,
+                                                           s),
+            "bf16_nt_v5": lambda: lib.vs_gemm_bf16_variant(5, 0, 1, n, n, n, 1.0, ah.data_ptr(), n,
+                                                           bh.data_ptr(), n, 0.0, c.data_ptr(), n,
+                                                           s),
             "torch_fp32": lambda: torch.matmul(a, b, out=c),
             "torch_bf16": lambda: torch.matmul(ah, bh),
         }
@@ -57,7 +65,7 @@ def main():
                 st = fn()
                 if isinstance(st, int) and st != 0:
                     raise RuntimeError(f"{k}: {lib.vs_last_error().decode()}")
-                if r == 0 and not k.startswith("torch"):
+                if r == 0 and not k.startswith("torch") and "_nt" not in k:
                     torch.cuda.synchronize()
                     errs[k] = (c[:128].double() - ref).abs().max().item()
                 e0.record()
