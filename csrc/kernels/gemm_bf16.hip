@@ -422,7 +422,52 @@ __device__ __forceinline__ bf16x8 gfrag(const uint8_t *img, int row, int c) {
   return *reinterpret_cast<const bf16x8 *>(img + row * C::RB + swz<C>(row, c) * 16);
 }
 
+// B read in place from its [K][N] storage (the NN layout, no transposing
+// prepass): the LDS image is [BK][BN] bf16 (k rows of BN * 2 bytes) filled
+// by the same lane-linear DMA, 16-byte chunk c of row k stored at chunk
+// c ^ ((k & 3) << 2), and the 32x32x16 B operand comes out of it
+// column-major through ds_read_b64_tr_b16 (cdna_hip_programming.md T10):
+// 16-lane group g (k rows 8 (g >> 1) + 0..3, then + 4..7, columns
+// 16 (g & 1) + 0..15), lane 4q + p addressing row q, columns 4p .. 4p + 3.
+// With the XOR each 32-lane half's 4 rows x 2 column blocks cover 64
+// distinct banks.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
 template <class C>
+__device__ __forceinline__ void dma_image_kn(const uint16_t *__restrict__ img, int64_t ld,
+                                             int col0, int k0, uint8_t *dst, int wave,
+                                             int lane) {
+  constexpr int RB = C::BN * 2, NCB = C::BN / 8, RPI = 1024 / RB;
+  static_assert(RB <= 1024 && 1024 % RB == 0 && NCB >= 16, "BN for the [K][N] image");
+#pragma unroll
+  for (int i = 0; i < C::kInstrB; i++) {
+    const int j = wave * C::kInstrB + i;
+    const int row = j * RPI + lane / NCB;
+    const int c = (lane % NCB) ^ ((row & 3) << 2);
+    const uint16_t *src = img + static_cast<int64_t>(k0 + row) * ld + col0 + 8 * c;
+    __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(dst + j * 1024), 16, 0,
+                                     0);
+  }
+}
+
+template <class C>
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t *img, int col0, int kb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int k = kb + 8 * (g >> 1) + q;
+  const auto at = [&](int kr) {
+    return (lds_v4i16 *)(img + kr * (C::BN * 2) + (((col >> 3) ^ ((kr & 3) << 2)) << 4) +
+                         (col & 7) * 2);
+  };
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(at(k));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(at(k + 4));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <class C, bool BKN = false>
 __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
   extern __shared__ __attribute__((aligned(1024))) uint8_t glds_lds[];
   constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
@@ -453,7 +498,8 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
 #pragma unroll
     for (int i = 0; i < NI; i++) {
       dma_image<C, C::kInstrA>(A[i], g.lda, m0, k0, img_a(buf, i), wid, lane);
-      dma_image<C, C::kInstrB>(B[i], g.ldb, n0, k0, img_b(buf, i), wid, lane);
+      if constexpr (BKN) dma_image_kn<C>(B[i], g.ldb, n0, k0, img_b(buf, i), wid, lane);
+      else dma_image<C, C::kInstrB>(B[i], g.ldb, n0, k0, img_b(buf, i), wid, lane);
     }
   };
 
@@ -481,7 +527,12 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
 #pragma unroll
         for (int x = 0; x < TM; x++) fa[i][x] = gfrag<C>(img_a(cur, i), arow + 32 * x, c);
 #pragma unroll
-        for (int y = 0; y < TN; y++) fb[i][y] = gfrag<C>(img_b(cur, i), brow + 32 * y, c);
+        for (int y = 0; y < TN; y++) {
+          if constexpr (BKN)
+            fb[i][y] = tr_frag<C>(img_b(cur, i), brow - lrow + 32 * y, 16 * ks, lane);
+          else
+            fb[i][y] = gfrag<C>(img_b(cur, i), brow + 32 * y, c);
+        }
       }
 #pragma unroll
       for (int x = 0; x < TM; x++)
@@ -521,13 +572,13 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     }
 }
 
-template <class C>
+template <class C, bool BKN = false>
 vs_status launch_glds(const Args &g, int batch, hipStream_t s) {
-  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_glds_kernel<C>),
+  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_glds_kernel<C, BKN>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes));
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
-  hipLaunchKernelGGL(gemm_glds_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
+  hipLaunchKernelGGL((gemm_glds_kernel<C, BKN>), dim3(tiles, 1, static_cast<unsigned>(batch)),
                      dim3(C::kThreads), C::kLdsBytes, s, g);
   VS_HIP(hipGetLastError());
   return VS_OK;
@@ -727,7 +778,9 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
     variant = t256 >= 256 ? 2 : (t256 >= 128 ? 1 : 0);
   }
-  VS_REQUIRE(variant >= 0 && variant <= 5, "gemm_bf16: unknown variant %d", variant);
+  VS_REQUIRE(variant >= 0 && variant <= 6, "gemm_bf16: unknown variant %d", variant);
+  const bool tr_variant = variant == 6;
+  if (tr_variant) variant = 2;
   int bm = variant == 1 ? 256 : 128, bn = 128, bk = kBK;
   if (variant == 2) {
     bm = split ? G3::BM : G1::BM;
@@ -758,7 +811,13 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
            (batch == 1 || st % 8 == 0) && reinterpret_cast<uintptr_t>(p) % 16 == 0;
   };
   const bool da = direct(ta == 0, m, mp, a, lda, sa);
-  const bool db = direct(tb != 0, n, np, b, ldb, sb);
+  // Variant 6: the two-stage LDS-DMA kernel with B read in place from [K][N]
+  // storage (tr-read image), i.e. NN without the transposing prepass.
+  // Measured slower than prepass + row reads (4096^3: 915 vs 933 TF, 8192^3:
+  // 983 vs 1108, profiles/r1/gemm_modes_v7_trread.log), so auto keeps the
+  // prepass; falls back to variant 2 when B is not a whole-tile [K][N] image.
+  const bool dbkn = tr_variant && direct(tb == 0, n, np, b, ldb, sb);
+  const bool db = dbkn || direct(tb != 0, n, np, b, ldb, sb);
   const size_t ea = static_cast<size_t>(mp) * kp, eb = static_cast<size_t>(np) * kp;
   const size_t wa = da ? 0 : ea * ni * batch, wb = db ? 0 : eb * ni * batch;
   DeviceBuffer buf;
@@ -800,6 +859,7 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   g.c = c;
   g.ldc = ldc;
   g.sc = sc;
+  if (dbkn) return launch_glds<G1, true>(g, batch, s);
   if (variant == 2) return split ? launch_glds<G3>(g, batch, s) : launch_glds<G1>(g, batch, s);
   if (variant == 3 || (variant >= 4 && split))
     return split ? launch_ring<R3>(g, batch, s) : launch_ring<R1>(g, batch, s);

@@ -45,6 +45,8 @@ def main():
                                                         bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
             "bf16_v4": lambda: lib.vs_gemm_bf16_variant(4, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
                                                         bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
+            "bf16_v6": lambda: lib.vs_gemm_bf16_variant(6, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
+                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
             "bf16_v5": lambda: lib.vs_gemm_bf16_variant(5, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
                                                         bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
             "bf16_nt_v2": lambda: lib.vs_gemm_bf16_variant(2, 0, 1, n, n, n, 1.0, ah.data_ptr(), n,

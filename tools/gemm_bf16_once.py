@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A few bf16 GEMM calls for counter collection: N^3 (env N, default 8192),
-NT layout (both operands read in place, no prepass), env VARIANT (default 2)."""
+NT layout by default (both operands read in place; TB=0: NN), env VARIANT
+(default 2)."""
 import ctypes
 import os
 import sys
@@ -12,13 +13,14 @@ from veles.simd_amd import _lib  # noqa: E402
 
 n = int(os.environ.get("N", "8192"))
 v = int(os.environ.get("VARIANT", "2"))
+tb = int(os.environ.get("TB", "1"))  # 0: NN (B stored [K][N])
 lib = _lib.lib()
 a = (torch.rand(n, n, device="cuda") - 0.5).bfloat16()
 b = (torch.rand(n, n, device="cuda") - 0.5).bfloat16()
 c = torch.empty(n, n, device="cuda")
 s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 for _ in range(int(os.environ.get("REPS", "5"))):
-    _lib.check(lib.vs_gemm_bf16_variant(v, 0, 1, n, n, n, 1.0, a.data_ptr(), n, b.data_ptr(),
+    _lib.check(lib.vs_gemm_bf16_variant(v, 0, tb, n, n, n, 1.0, a.data_ptr(), n, b.data_ptr(),
                                         n, 0.0, c.data_ptr(), n, s), "bf16")
 torch.cuda.synchronize()
 print("ok")
