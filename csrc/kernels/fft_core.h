@@ -1,8 +1,8 @@
 // LDS-resident Stockham FFT building blocks for CDNA4.
 //
 // One signal of N = 2^LOGN complex points (N <= 16384) lives in LDS
-// (float2, one pad slot per 16 elements to break the power-of-two strides
-// of the early passes) while TPS = N/E threads each own E = 16 (32 at
+// (float2, XOR-swizzled within 16-element rows -- see lds_slot -- so the
+// power-of-two strides of the exchanges hit distinct banks) while TPS = N/E threads each own E = 16 (32 at
 // N = 16384) points in registers.  Each pass is a radix-R Stockham step (R in {2,4,8,16}):
 //   butterfly i in [0, N/R), k = i mod P (P = product of earlier radices):
 //     u_j = x[i + j N/R] * w^(j k),  w = exp(-+2 pi i / (P R))
@@ -183,8 +183,20 @@ __device__ __forceinline__ void dft(float2 *v) {
   else dft32<INV>(v);
 }
 
-// LDS index with one pad slot per 16 complex elements.
-__device__ __forceinline__ int pad(int e) { return e + (e >> 4); }
+// LDS slot of complex element e: bits 0-3 XORed with bits 4-7 ^ 8-11, a
+// bijection on every 16-aligned block (no padding).  The exchanges move
+// float2 with ds_write_b64 (lane groups of 16, bank = slot mod 16 pairs)
+// and ds_read_b64 (groups of 32, bank = slot mod 32 pairs;
+// MI355X_MICROARCH.md §LDS).  Reads take 32 consecutive aligned e: the XOR
+// permutes within each 16-half and bit 4 keeps the halves apart -> 32
+// distinct.  Writes e = (i - k) R + k + j P over 16 consecutive lanes i:
+// P >= 16 gives 16 consecutive k with bits >= 4 fixed; P = 1 gives stride R,
+// whose lane bits land in e's bits 4-7 (R = 16), or bits 5-8 (R = 32, the
+// e >> 8 term separates lanes i and i + 8), or are split between bits 0-3
+// and 4-7 (R <= 8): all 16 distinct.  The previous "one pad slot per 16"
+// layout put slots 0 and 32 of every 32-element read in one bank (2-way
+// conflicts on every read) and 2-way on the radix-32 P = 1 writes.
+__device__ __forceinline__ int lds_slot(int e) { return e ^ (((e >> 4) ^ (e >> 8)) & 15); }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a full
 // workgroup fence: every wave drains vmcnt at every LDS exchange, i.e. waits
@@ -261,7 +273,10 @@ struct Plan {
   // fewer LDS round trips and barriers.
   static constexpr bool R32 = LOGN == 14;
   static constexpr int NPASS = R32 ? 3 : (LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1);
-  static constexpr int kLds = N + N / 16 + 1;      // per-signal LDS (float2)
+  // per-signal LDS (float2).  Signals narrower than a 32-lane read group
+  // (TPS < 32, several per wave) are TPS slots apart so their aligned
+  // TPS-slot read blocks land in different banks.
+  static constexpr int kLds = N + (TPS < 32 ? TPS : 0);
   // Radix of pass q (forward order: the odd radix first).
   static constexpr int radix(int q) {
     if (R32) return q == 0 ? 16 : 32;
@@ -332,7 +347,7 @@ struct Pass {
           const int k = i & (P - 1);
           const int base = (i - k) * R + k;
 #pragma unroll
-          for (int j = 0; j < R; j++) lds[pad(base + j * P)] = comp(v[b * R + j]);
+          for (int j = 0; j < R; j++) lds[lds_slot(base + j * P)] = comp(v[b * R + j]);
         }
       };
       // LDS -> the next pass's inputs, element e of v via `sink(e, value)`
@@ -341,7 +356,7 @@ struct Pass {
         for (int b = 0; b < PL::E / R2; b++) {
           const int i = t + b * PL::TPS;
 #pragma unroll
-          for (int j = 0; j < R2; j++) sink(b * R2 + j, lds[pad(i + j * (PL::N / R2))]);
+          for (int j = 0; j < R2; j++) sink(b * R2 + j, lds[lds_slot(i + j * (PL::N / R2))]);
         }
       };
       if constexpr (std::is_same_v<LT, float2>) {
