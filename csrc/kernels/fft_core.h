@@ -28,23 +28,29 @@
 namespace vs {
 namespace fft {
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) {
-  return make_float2(a.x + b.x, a.y + b.y);
-}
-__device__ __forceinline__ float2 csub(float2 a, float2 b) {
-  return make_float2(a.x - b.x, a.y - b.y);
-}
+// Complex helpers written as 2-lane vector arithmetic with lane shuffles so
+// each maps onto one or two v_pk_*_f32 with op_sel / neg modifiers (no
+// register-pair shuffling between packed and scalar halves).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v to_v(float2 a) { return f2v{a.x, a.y}; }
+__device__ __forceinline__ float2 from_v(f2v a) { return make_float2(a.x, a.y); }
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return from_v(to_v(a) + to_v(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return from_v(to_v(a) - to_v(b)); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  const f2v av = to_v(a), bv = to_v(b);
+  return from_v(av.xx * bv + av.yy * (bv.yx * f2v{-1.f, 1.f}));
 }
 // a * conj(b)
 __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
-  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+  const f2v av = to_v(a), bv = to_v(b);
+  return from_v(av * bv.xx + av.yx * (bv.yy * f2v{1.f, -1.f}));
 }
 // z * (-i) forward, z * (+i) inverse
 template <bool INV>
 __device__ __forceinline__ float2 rot90(float2 z) {
-  return INV ? make_float2(-z.y, z.x) : make_float2(z.y, -z.x);
+  const f2v v = to_v(z).yx;
+  return from_v(INV ? v * f2v{-1.f, 1.f} : v * f2v{1.f, -1.f});
 }
 
 template <bool INV>
@@ -74,16 +80,16 @@ constexpr float kC8 = 0.70710678118654752440f;   // cos(pi/4)
 constexpr float kC16 = 0.92387953251128675613f;  // cos(pi/8)
 constexpr float kS16 = 0.38268343236508977173f;  // sin(pi/8)
 
-// z * exp(-+ i pi/4) and z * exp(-+ 3 i pi/4)
+// z * exp(-+ i pi/4) and z * exp(-+ 3 i pi/4): kC8 (z +- rot90(z))
 template <bool INV>
 __device__ __forceinline__ float2 w8_1(float2 z) {
-  return INV ? make_float2(kC8 * (z.x - z.y), kC8 * (z.x + z.y))
-             : make_float2(kC8 * (z.x + z.y), kC8 * (z.y - z.x));
+  const f2v v = to_v(z), r = to_v(rot90<INV>(z));
+  return from_v((v + r) * kC8);
 }
 template <bool INV>
 __device__ __forceinline__ float2 w8_3(float2 z) {
-  return INV ? make_float2(-kC8 * (z.x + z.y), kC8 * (z.x - z.y))
-             : make_float2(kC8 * (z.y - z.x), -kC8 * (z.x + z.y));
+  const f2v v = to_v(z), r = to_v(rot90<INV>(z));
+  return from_v((r - v) * kC8);
 }
 
 template <bool INV>
