@@ -28,9 +28,9 @@ step() {  # step <name> <timeout> <cmd...>
 rocm-smi --showproductname > "$OUT/device.txt" 2>&1 || true
 if [ "$MODE" = "tests" ] || [ "$MODE" = "all" ]; then
   if [ -n "$KEXPR" ]; then
-    step pytest_gpu 900 python -m pytest tests -m gpu -q -x -k "$KEXPR"
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "$KEXPR"
   else
-    step pytest_gpu 900 python -m pytest tests -m gpu -q
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
   fi
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
