@@ -120,8 +120,16 @@ size_t gpu_min_elems() {
 }
 
 unsigned elementwise_grid(size_t work_items, unsigned block) {
-  // 256 CUs x 8 resident 256-thread blocks; grid-stride the rest.
-  const size_t cap = 2048;
+  // One work item per thread up to 2^20 blocks (2^28 threads), grid-stride
+  // beyond.  Measured on 2^26-element fp32 maps: a 2048-block grid-stride
+  // grid reaches 5.0-5.6 TB/s, one item per thread 5.9-6.2 TB/s
+  // (profiles/r1/session5/elementwise_grid_cap_ab.md).  VS_EW_GRID_CAP
+  // overrides the cap for tuning runs.
+  static const size_t cap = [] {
+    const char *e = std::getenv("VS_EW_GRID_CAP");
+    const size_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v ? v : size_t{1} << 20;
+  }();
   size_t g = (work_items + block - 1) / block;
   if (g > cap) g = cap;
   if (g == 0) g = 1;

@@ -19,7 +19,10 @@ except Exception:  # pragma: no cover - torch is present in every supported env
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_native", "libvelessimd.so")
+# VELES_SIMD_LIB points at an alternative build (A/B runs of two kernel
+# variants in one GPU session); default is the in-tree library.
+LIB_PATH = os.environ.get("VELES_SIMD_LIB") or os.path.join(
+    _HERE, "_native", "libvelessimd.so")
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 _vp = ctypes.c_void_p
