@@ -125,10 +125,22 @@ unsigned elementwise_grid(size_t work_items, unsigned block) {
   // grid reaches 5.0-5.6 TB/s, one item per thread 5.9-6.2 TB/s
   // (profiles/r1/session5/elementwise_grid_cap_ab.md).  VS_EW_GRID_CAP
   // overrides the cap for tuning runs.
-  static const size_t cap = [] {
+  static const size_t cap = [block] {
+    // HIP limits gridDim.x * blockDim.x to < 2^32 threads.
+    const size_t hw_max = (size_t{0xffffffffu}) / (block ? block : 256);
     const char *e = std::getenv("VS_EW_GRID_CAP");
-    const size_t v = e ? std::strtoull(e, nullptr, 10) : 0;
-    return v ? v : size_t{1} << 20;
+    if (!e) return size_t{1} << 20;
+    char *end = nullptr;
+    const unsigned long long v = std::strtoull(e, &end, 10);
+    if (end == e || *end != '\0' || v == 0) {
+      std::fprintf(stderr, "veles.simd: ignoring VS_EW_GRID_CAP=%s (not a positive integer)\n", e);
+      return size_t{1} << 20;
+    }
+    if (v > hw_max) {
+      std::fprintf(stderr, "veles.simd: VS_EW_GRID_CAP=%llu clamped to %zu\n", v, hw_max);
+      return hw_max;
+    }
+    return static_cast<size_t>(v);
   }();
   size_t g = (work_items + block - 1) / block;
   if (g > cap) g = cap;

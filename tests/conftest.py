@@ -13,7 +13,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running test")
     # Build the native library once if this checkout does not have it yet.
     from veles.simd_amd import _lib, build
-    if not os.path.exists(_lib.LIB_PATH):
+    if os.environ.get("VELES_SIMD_LIB"):
+        # An explicit override is never rebuilt: fail fast and say which path.
+        if not os.path.exists(_lib.LIB_PATH):
+            raise pytest.UsageError(
+                f"VELES_SIMD_LIB={_lib.LIB_PATH} does not exist")
+    elif not os.path.exists(_lib.LIB_PATH):
         build.build()
 
 

@@ -18,6 +18,12 @@ step() {  # step <name> <timeout> <cmd...>
   local rc=$?
   echo "=== $name rc=$rc"
   tail -n 25 "$OUT/$name.log"
+  # pytest-timeout's thread method ends a hung test with os._exit(1): rc 1
+  # then means "GPU possibly stuck", not "tests failed".
+  if grep -q '+++ Timeout +++' "$OUT/$name.log"; then
+    echo "!!! $name hit a per-test timeout (possible GPU hang): stopping the session"
+    exit 124
+  fi
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
     echo "!!! $name ended with rc=$rc: stopping the session"
     exit $rc
