@@ -73,3 +73,12 @@ asan:
 	    -L$(ASAN_BUILD)/lib -lvelessimd -Wl,-rpath,'$$ORIGIN/../lib'
 
 .PHONY: asan
+
+# Diagnostic build: per-phase s_memtime stamps in the real-block conv kernel
+# (tools/conv_stamps.py).  Not the shipped library.
+STAMPS_BUILD := build-stamps
+stamps:
+	$(MAKE) BUILD=$(STAMPS_BUILD) OPT="-O3 -DVS_CONV_STAMPS" \
+	    LIBDIR=$(STAMPS_BUILD)/lib LIB=$(STAMPS_BUILD)/lib/libvelessimd.so lib
+
+.PHONY: stamps

@@ -34,12 +34,17 @@
 
 namespace vs {
 namespace conv {
-extern int g_conv_buf, g_conv_split;  // tuning knobs, defined below
+extern int g_conv_buf, g_conv_split, g_conv_real, g_conv_real_all;  // tuning knobs, defined below
 namespace {
 
 using fft::cmul;
 using fft::Plan;
 using fft::reg_index;
+
+// smallest real-block transform (L = 2^kRealMinLog real samples, M = L / 2)
+constexpr int kRealMinLog = 7;
+// taps per partition of a filter too long for one overlap-save block
+constexpr int kPartTaps = 4096;
 
 // ------------------------------------------------------------- direct
 constexpr int kDirThreads = 256;
@@ -381,6 +386,329 @@ void launch_block_t(const BlockArgs &a, const float2 *tw, hipStream_t s) {
 }
 
 
+// Diagnostic build only (-DVS_CONV_STAMPS, tools/conv_stamps.py): per-phase
+// shader-clock stamps of wave 0 of every real-block workgroup, read back by
+// vs_conv_stamps().  Never compiled into the shipped library.
+#ifdef VS_CONV_STAMPS
+constexpr int kStampSlots = 8, kStampMax = 1 << 16;
+__device__ unsigned long long g_stamps[kStampMax * kStampSlots];
+#define VS_STAMP(i) stamp[i] = __builtin_amdgcn_s_memtime()
+// Residency probe: every 256-thread workgroup sleeps ~`spin` shader cycles;
+// VG forces the kernel to allocate >= VG VGPRs.  Elapsed time / (blocks per
+// CU x spin) tells how many workgroups the hardware keeps resident per CU.
+template <int VG>
+__global__ __launch_bounds__(256) void residency_kernel(float *out, long long spin) {
+  extern __shared__ float dyn[];
+  if constexpr (VG == 240) asm volatile("v_mov_b32 v239, 0" ::: "v239");
+  if constexpr (VG == 168) asm volatile("v_mov_b32 v167, 0" ::: "v167");
+  if constexpr (VG == 128) asm volatile("v_mov_b32 v127, 0" ::: "v127");
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  while (__builtin_amdgcn_s_memtime() - t0 < spin) __builtin_amdgcn_s_sleep(8);
+  dyn[threadIdx.x] = threadIdx.x;
+  __syncthreads();
+  if (blockIdx.x == 0) out[threadIdx.x] = dyn[255 - threadIdx.x];
+}
+
+#else
+#define VS_STAMP(i)
+#endif
+
+// --------------------------------------- real-block fused convolution
+// One workgroup per block of L = 2M real samples, transformed as an M-point
+// complex FFT of z[m] = x[2m] + i x[2m+1].  The real-spectrum split, the
+// filter product and the inverse merge are one linear map per bin pair
+// (k, M - k):
+//   Z'[k] = P[k] Z[k] + Q[k] conj(Z[M - k])        (real_filter_kernel)
+// so the spectrum step is one LDS exchange (each thread reads the mirror
+// bin of each of its own bins) and two complex products.  An M = 8192
+// transform (L = 16384, the overlap-save block of a 4096-tap filter) needs
+// 64 KiB of LDS: two workgroups per CU, so one's HBM loads / stores and LDS
+// exchanges overlap the other's butterflies -- the pair kernel above keeps a
+// 16384-point complex image (128 KiB, one workgroup per CU) and serialises
+// them.
+struct RealArgs {
+  const float *x;
+  int64_t xs;
+  int xlen;
+  float *y;      // this pass's output origin (row 0, sample 0)
+  int64_t ys;
+  int ylen;      // outputs of this pass per row
+  int yroom;     // writable samples from y per row (>= ylen)
+  const float4 *PQ;  // {P, Q}, M per filter
+  int pq_per_signal;
+  int pre;       // history samples per block (taps - 1 for overlap-save)
+  int step;      // valid outputs per block
+  int nblk;      // blocks per signal
+  int accumulate;  // y += result (partitioned long filters)
+};
+
+template <class PL, bool BUF>
+__device__ __forceinline__ void load_real(const RealArgs &a, const float *xr, int st, int t,
+                                          float2 (&v)[PL::E]) {
+  constexpr int R0 = PL::first_radix(false);
+  if (BUF && st >= 0) {
+    // 8-byte buffer loads; the range check zeroes samples past the row
+    // (checked per dword: tests/test_convolve.py odd lengths)
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(xr), 0, 4 * a.xlen,
+                                                     0x00020000);
+    const int o = 4 * (st + 2 * t);
+#pragma unroll
+    for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+      for (int j = 0; j < R0; j++) {
+        const int d = 8 * reg_index<PL, R0>(0, b, j);
+        const auto w = __builtin_amdgcn_raw_buffer_load_b64(r, o + d, 0, 0);
+        v[b * R0 + j] = make_float2(__uint_as_float(w[0]), __uint_as_float(w[1]));
+      }
+  } else {
+    const int last = a.xlen - 1;
+#pragma unroll
+    for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+      for (int j = 0; j < R0; j++) {
+        const int p = st + 2 * reg_index<PL, R0>(t, b, j);
+        const float u0 = xr[min(max(p, 0), last)];
+        const float u1 = xr[min(max(p + 1, 0), last)];
+        v[b * R0 + j] = make_float2(static_cast<unsigned>(p) <= static_cast<unsigned>(last) ? u0 : 0.f,
+                                    static_cast<unsigned>(p + 1) <= static_cast<unsigned>(last) ? u1 : 0.f);
+      }
+  }
+}
+
+template <class PL, bool BUF>
+__device__ __forceinline__ void store_real(const RealArgs &a, float *yr, int st, int t,
+                                           const float2 (&v)[PL::E]) {
+  constexpr int R0 = PL::radix(0);  // last pass of the reversed-radix inverse
+  // valid block positions [lo, hi): history dropped, row end respected
+  const int lo = a.pre, hi = min(a.pre + a.step, a.ylen - st);
+  const auto w = __builtin_amdgcn_make_buffer_rsrc(yr, 0, BUF ? 4 * a.yroom : 0, 0x00020000);
+#pragma unroll
+  for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+    for (int j = 0; j < R0; j++) {
+      const int p = 2 * reg_index<PL, R0>(t, b, j);
+      float2 r = v[b * R0 + j];
+      const bool ok0 = p >= lo && p < hi, ok1 = p + 1 >= lo && p + 1 < hi;
+      if constexpr (BUF) {
+        const int off = 4 * (st + p);
+        if (ok0 && ok1) {
+          if (a.accumulate) {
+            const auto o = __builtin_amdgcn_raw_buffer_load_b64(w, off, 0, 0);
+            r.x += __uint_as_float(o[0]);
+            r.y += __uint_as_float(o[1]);
+          }
+          __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(r.x),
+                                                             __float_as_uint(r.y)};
+          __builtin_amdgcn_raw_buffer_store_b64(u, w, off, 0, 0);
+        } else if (ok0 || ok1) {
+          const int o1 = ok0 ? off : off + 4;
+          float q = ok0 ? r.x : r.y;
+          if (a.accumulate) q += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w, o1, 0, 0));
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(q), w, o1, 0, 0);
+        }
+      } else {
+        float *dst = yr + st + p;
+        if (ok0) dst[0] = a.accumulate ? dst[0] + r.x : r.x;
+        if (ok1) dst[1] = a.accumulate ? dst[1] + r.y : r.y;
+      }
+    }
+}
+
+// Spectrum step of real_conv_kernel on elements [C0, C0 + CN) of v (pattern
+// reg_index<RL>): Z'[k] = P[k] Z[k] + Q[k] conj(Z[M - k]).
+template <class PL, int C0, int CN>
+__device__ __forceinline__ void real_spectrum_chunk(float2 (&v)[PL::E], const float2 *lds,
+                                                    const float4 (&pq)[CN], int t) {
+  constexpr int RL = PL::last_radix(false);
+#pragma unroll
+  for (int c = 0; c < CN; c++) {
+    const int e = C0 + c;
+    const int k = reg_index<PL, RL>(t, e / RL, e % RL);
+    const float2 zm = lds[fft::lds_slot((PL::N - k) & (PL::N - 1))];
+    v[e] = fft::cadd(cmul(make_float2(pq[c].x, pq[c].y), v[e]),
+                     fft::cmulc(make_float2(pq[c].z, pq[c].w), zm));
+  }
+}
+
+template <class PL, int C0, int CN>
+__device__ __forceinline__ void real_pq_load(const float4 *__restrict__ PQ, int t,
+                                             float4 (&pq)[CN]) {
+  constexpr int RL = PL::last_radix(false);
+#pragma unroll
+  for (int c = 0; c < CN; c++) {
+    const int e = C0 + c;
+    pq[c] = PQ[reg_index<PL, RL>(t, e / RL, e % RL)];
+  }
+}
+
+// Every global load of this kernel is issued ahead of its use: the input
+// block and the forward twiddles (RegTw) at entry, the P / Q table in
+// chunks one chunk ahead of the products, the inverse twiddles before the
+// spectrum exchange -- TableTw / plain indexing waited for each L2 hit
+// right before its use (32 serial P / Q round trips per block).
+template <int LOGM, int EP, bool BUF>
+__global__ __launch_bounds__((Plan<LOGM, EP>::TPS)) void real_conv_kernel(
+    RealArgs a, const float2 *__restrict__ tw) {
+  using PL = Plan<LOGM, EP>;
+  constexpr int E = PL::E;
+  constexpr int CH = E / 4;  // P / Q chunk (elements)
+  __shared__ float2 lds[PL::N];
+  const int t = threadIdx.x;
+  // grid = (blocks per signal, signals): both indices stay in SGPRs (a
+  // buffer descriptor built from a VALU-divided index turned every load
+  // into a waterfall loop)
+  const int sig = blockIdx.y;
+  const int blk = blockIdx.x;
+  const float *xr = a.x + static_cast<long long>(sig) * a.xs;
+  float *yr = a.y + static_cast<long long>(sig) * a.ys;
+  const int st = blk * a.step - a.pre;
+#ifdef VS_CONV_STAMPS
+  unsigned long long stamp[kStampSlots] = {};
+#endif
+  VS_STAMP(0);
+  float2 v[E];
+  load_real<PL, BUF>(a, xr, st, t, v);
+  fft::RegTw<PL, false> twf;
+  twf.load(t, tw);
+  __builtin_amdgcn_sched_barrier(0);
+  VS_STAMP(1);
+  fft::transform<PL, false, false>(v, lds, t, twf);
+  VS_STAMP(2);
+  // v: Z[k], k = reg_index<RL>; the inverse starts from the same pattern
+  constexpr int RL = PL::last_radix(false);
+  const float4 *PQ = a.PQ + (a.pq_per_signal ? static_cast<long long>(sig) * PL::N : 0);
+  float4 pq0[CH], pq1[CH];
+  real_pq_load<PL, 0, CH>(PQ, t, pq0);
+  fft::RegTw<PL, true> twi;
+  twi.load(t, tw);
+#pragma unroll
+  for (int b = 0; b < E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++)
+      lds[fft::lds_slot(reg_index<PL, RL>(t, b, j))] = v[b * RL + j];
+  fft::lds_barrier();
+  real_pq_load<PL, CH, CH>(PQ, t, pq1);
+  __builtin_amdgcn_sched_barrier(0);
+  real_spectrum_chunk<PL, 0, CH>(v, lds, pq0, t);
+  real_pq_load<PL, 2 * CH, CH>(PQ, t, pq0);
+  __builtin_amdgcn_sched_barrier(0);
+  real_spectrum_chunk<PL, CH, CH>(v, lds, pq1, t);
+  real_pq_load<PL, 3 * CH, CH>(PQ, t, pq1);
+  __builtin_amdgcn_sched_barrier(0);
+  real_spectrum_chunk<PL, 2 * CH, CH>(v, lds, pq0, t);
+  __builtin_amdgcn_sched_barrier(0);
+  real_spectrum_chunk<PL, 3 * CH, CH>(v, lds, pq1, t);
+  fft::lds_barrier();
+  VS_STAMP(3);
+  fft::transform<PL, true, true>(v, lds, t, twi);
+  VS_STAMP(4);
+  store_real<PL, BUF>(a, yr, st, t, v);
+#ifdef VS_CONV_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  VS_STAMP(5);
+  if (threadIdx.x < 64) {
+    unsigned hw = 0, xcc = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    stamp[6] = hw;
+    stamp[7] = xcc;
+    const long long wg = static_cast<long long>(blockIdx.y) * gridDim.x + blockIdx.x;
+    const int lane = threadIdx.x;
+    if (wg < kStampMax && lane < kStampSlots) {
+      unsigned long long val = 0;
+#pragma unroll
+      for (int i = 0; i < kStampSlots; i++)
+        if (lane == i) val = stamp[i];
+      g_stamps[wg * kStampSlots + lane] = val;
+    }
+  }
+#endif
+}
+
+// P, Q of the real-block kernel, one launch per filter straight from the
+// taps: the zero-padded (optionally reversed) filter of L = 2M samples as an
+// M-point complex transform of its even/odd pairs Zh, then the real split
+//   H[k] = a Zh[k] + b conj(Zh[M-k]),  H[M-k] = conj(a) Zh[M-k] + conj(b) conj(Zh[k])
+// and the fold
+//   a = (1 - i W^k)/2, b = (1 + i W^k)/2   (split:  X[k] = a Z[k] + b Z*[M-k])
+//   c = conj(a), d = conj(b)               (merge:  Z'[k] = c Y[k] + d Y*[M-k])
+//   P = (c a H[k] + d b H*[M-k]) / M,  Q = (c b H[k] + d a H*[M-k]) / M
+// with W = exp(-2 pi i / L) (k = 0 pairs with itself: H[M] is the Nyquist bin).
+template <int LOGM, int EP>
+__global__ __launch_bounds__((Plan<LOGM, EP>::TPS)) void real_filter_kernel(
+    const float *__restrict__ h, int hlen, int64_t hs, int reverse,
+    const float2 *__restrict__ tw, const float2 *__restrict__ twl, float4 *__restrict__ PQ) {
+  using PL = Plan<LOGM, EP>;
+  __shared__ float2 lds[PL::N];
+  const int t = threadIdx.x;
+  const float *hr = h + static_cast<long long>(blockIdx.x) * hs;
+  constexpr int R0 = PL::first_radix(false);
+  float2 v[PL::E];
+#pragma unroll
+  for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+    for (int j = 0; j < R0; j++) {
+      const int n = 2 * reg_index<PL, R0>(t, b, j);
+      const float u0 = n < hlen ? hr[reverse ? hlen - 1 - n : n] : 0.f;
+      const float u1 = n + 1 < hlen ? hr[reverse ? hlen - 2 - n : n + 1] : 0.f;
+      v[b * R0 + j] = make_float2(u0, u1);
+    }
+  fft::transform<PL, false, false>(v, lds, t, tw);
+  constexpr int RL = PL::last_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++)
+      lds[fft::lds_slot(reg_index<PL, RL>(t, b, j))] = v[b * RL + j];
+  fft::lds_barrier();
+  float4 *out = PQ + static_cast<long long>(blockIdx.x) * PL::N;
+  const float sc = 1.0f / static_cast<float>(PL::N);
+#pragma unroll
+  for (int b = 0; b < PL::E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+      const int k = reg_index<PL, RL>(t, b, j);
+      const float2 zk = v[b * RL + j];
+      const float2 zm = lds[fft::lds_slot((PL::N - k) & (PL::N - 1))];
+      const float2 w = twl[k];                   // W^k, W = exp(-2 pi i / L)
+      const float2 iw = make_float2(-w.y, w.x);  // i W^k
+      const float2 ca = make_float2(0.5f * (1.f - iw.x), -0.5f * iw.y);
+      const float2 cb = make_float2(0.5f * (1.f + iw.x), 0.5f * iw.y);
+      const float2 zmc = make_float2(zm.x, -zm.y);
+      const float2 hk = fft::cadd(cmul(ca, zk), cmul(cb, zmc));
+      // conj(H[M-k]) = a conj(Zh[M-k]) + b Zh[k]
+      const float2 hm = fft::cadd(cmul(ca, zmc), cmul(cb, zk));
+      const float2 cc = make_float2(ca.x, -ca.y);  // (1 + i W^-k)/2 = conj(a)
+      const float2 cd = make_float2(cb.x, -cb.y);  // (1 - i W^-k)/2 = conj(b)
+      const float2 P = fft::cadd(cmul(cmul(cc, ca), hk), cmul(cmul(cd, cb), hm));
+      const float2 Q = fft::cadd(cmul(cmul(cc, cb), hk), cmul(cmul(cd, ca), hm));
+      out[k] = make_float4(sc * P.x, sc * P.y, sc * Q.x, sc * Q.y);
+    }
+}
+
+template <int LOGM, int EP>
+vs_status run_real_t(int correlate, const float *h, int hlen, int64_t hs, int nfilt,
+                     RealArgs a, long long nblocks, hipStream_t s) {
+  using PL = Plan<LOGM, EP>;
+  vs_status st;
+  const float2 *tw = fft::twiddles(LOGM, &st);
+  if (!tw) return st;
+  const float2 *twl = fft::twiddles(LOGM + 1, &st);
+  if (!twl) return st;
+  DeviceBuffer pq;
+  VS_TRY(pq.alloc(sizeof(float4) * PL::N * static_cast<size_t>(nfilt), s));
+  hipLaunchKernelGGL((real_filter_kernel<LOGM, EP>), dim3(static_cast<unsigned>(nfilt)),
+                     dim3(PL::TPS), 0, s, h, hlen, hs, correlate, tw, twl, pq.as<float4>());
+  a.PQ = pq.as<float4>();
+  const dim3 grid(static_cast<unsigned>(a.nblk), static_cast<unsigned>(nblocks / a.nblk));
+  if (g_conv_buf && a.xlen < (1 << 29) && a.yroom < (1 << 29))
+    hipLaunchKernelGGL((real_conv_kernel<LOGM, EP, true>), grid, dim3(PL::TPS), 0, s, a, tw);
+  else
+    hipLaunchKernelGGL((real_conv_kernel<LOGM, EP, false>), grid, dim3(PL::TPS), 0, s, a, tw);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
 // ------------------------------------------ large FFT path (four-step)
 // z[p][n] = x[2p][n] + i x[2p+1][n] (zero padded to 2^logm)
 __global__ __launch_bounds__(256) void pack_pairs_kernel(
@@ -438,6 +766,13 @@ int g_conv_buf = 1;
 // Tuning knob (vs_tune_set("conv_split", 0/1)): 16384-point block kernel with
 // the split (real, then imaginary) LDS exchange, two workgroups per CU.
 int g_conv_split = 0;
+// Tuning knob (vs_tune_set("conv_real", 0/1/2)): real-block kernel for the
+// overlap-save / single-block paths (0: pair kernel; 2: 16 points per thread
+// at M = 8192 instead of 32).
+int g_conv_real = 1;
+// Tuning knob (vs_tune_set("conv_real_all", 0/1)): real-block kernel for
+// every block size (default: L >= 8192 only, see use_real).
+int g_conv_real_all = 0;
 
 int os_block_log(int hlen) {
   // Reference block size 2^(floor(log2 M) + 2) (src/convolve.c:116-121),
@@ -466,7 +801,9 @@ int select(int xlen, int hlen, int batch) {
   if (lm <= fft::kMaxLdsLog && (!os_ok || ylen <= (1LL << los)))
     return VS_CONV_FFT;  // one block covers the whole output
   if (os_ok) return VS_CONV_OVERLAP_SAVE;
-  return VS_CONV_FFT;
+  // Long filter: one padded transform while it exists, else partitioned
+  // overlap-save (vs_conv1d never fails for a valid shape).
+  return lm <= fft::kMaxLog ? VS_CONV_FFT : VS_CONV_OVERLAP_SAVE;
 }
 
 vs_status run_direct(int correlate, const float *x, int xlen, int64_t xs,
@@ -551,6 +888,92 @@ vs_status run_block(int correlate, bool overlap_save, const float *x, int xlen,
   return VS_OK;
 }
 
+// Real-block kernel or pair kernel for blocks of 2^logl samples.  Measured
+// at x = 2^20, batch 64 (profiles/r2/conv_real_ab.md): the real-block kernel
+// wins from L = 4096 on (1500 taps: 302 vs 288 Gsamples/s; 3000: 303 vs
+// 228; 4096: 262 vs 242), the pair kernel at
+// L = 2048 (1000 taps: 296 vs 284) where both stay L2-resident and the
+// pair kernel skips the spectrum exchange.
+bool use_real(int logl) {
+  if (g_conv_real == 0 || logl < kRealMinLog) return false;
+  return g_conv_real == 2 || logl >= 12 || g_conv_real_all;
+}
+
+// Real-block path (real_conv_kernel): blocks of L = 2^logl real samples.
+// `ylen` outputs per row land at y (row stride ys, `yroom` writable samples
+// per row from y); accumulate adds them to what is there.
+vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, int64_t xs,
+                   const float *h, int hlen, int64_t hs, float *y, int64_t ys, int ylen,
+                   int yroom, int accumulate, int batch, hipStream_t s) {
+  int logl;
+  if (overlap_save) {
+    logl = os_block_log(hlen);
+  } else {
+    logl = kRealMinLog;
+    while ((1LL << logl) < ylen) logl++;
+  }
+  VS_REQUIRE(logl >= kRealMinLog && logl <= fft::kMaxLdsLog,
+             "real-block convolution: block 2^%d out of range", logl);
+  const int L = 1 << logl;
+  RealArgs a{};
+  a.x = x;
+  a.xs = xs;
+  a.xlen = xlen;
+  a.y = y;
+  a.ys = ys;
+  a.ylen = ylen;
+  a.yroom = yroom;
+  a.pq_per_signal = hs != 0;
+  a.pre = overlap_save ? hlen - 1 : 0;
+  a.step = L - a.pre;
+  VS_REQUIRE(a.step > 0 && hlen <= L, "real-block convolution: filter (%d) longer than the block (%d)",
+             hlen, L);
+  a.nblk = (ylen + a.step - 1) / a.step;
+  a.accumulate = accumulate;
+  const long long nblocks = static_cast<long long>(a.nblk) * batch;
+  VS_REQUIRE(batch <= kMaxGridY, "real-block convolution: batch %d > %lld per launch", batch,
+             kMaxGridY);
+  const int nfilt = hs ? batch : 1;
+  switch (logl - 1) {
+#define VS_CASE(LG, EP) \
+  case LG: return run_real_t<LG, EP>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
+    VS_CASE(6, 0) VS_CASE(7, 0) VS_CASE(8, 0) VS_CASE(9, 0) VS_CASE(10, 0) VS_CASE(11, 0)
+    VS_CASE(12, 0)
+#undef VS_CASE
+    case 13:
+      if (g_conv_real == 2)
+        return run_real_t<13, 16>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
+      return run_real_t<13, 32>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
+  }
+  set_error("real-block convolution: unsupported block 2^%d", logl);
+  return VS_ERR_UNSUPPORTED;
+}
+
+// Filters too long for one overlap-save block: partitions of kPartTaps taps,
+// each an overlap-save pass whose outputs are added at the partition's
+// offset, y = sum_p (x * h_p)[n - p kPartTaps].  Correlation partitions the
+// reversed filter (partition p of it is h[hlen - p P - len_p, ...) reversed).
+vs_status run_partitioned(int correlate, const float *x, int xlen, int64_t xs,
+                          const float *h, int hlen, int64_t hs, float *y, int64_t ys,
+                          int batch, hipStream_t s) {
+  const int ylen = xlen + hlen - 1;
+  // the first pass writes [0, xlen + kPartTaps - 1); later passes add into
+  // the rest of the row, which starts at zero
+  const int head = xlen + std::min(kPartTaps, hlen) - 1;
+  if (head < ylen)
+    VS_HIP(hipMemset2DAsync(y + head, static_cast<size_t>(ys) * sizeof(float), 0,
+                            static_cast<size_t>(ylen - head) * sizeof(float),
+                            static_cast<size_t>(batch), s));
+  for (int p0 = 0, part = 0; p0 < hlen; p0 += kPartTaps, part++) {
+    const int len = std::min(kPartTaps, hlen - p0);
+    const float *hp = correlate ? h + (hlen - p0 - len) : h + p0;
+    log(2, "vs_conv1d: partition %d taps [%d, %d)", part, p0, p0 + len);
+    VS_TRY(run_real(correlate, true, x, xlen, xs, hp, len, hs, y + p0, ys, xlen + len - 1,
+                    ylen - p0, part > 0, batch, s));
+  }
+  return VS_OK;
+}
+
 vs_status run_fft_large(int correlate, const float *x, int xlen, int64_t xs,
                         const float *h, int hlen, int64_t hs, float *y, int64_t ys,
                         int batch, hipStream_t s) {
@@ -564,16 +987,9 @@ vs_status run_fft_large(int correlate, const float *x, int xlen, int64_t xs,
   const long long M = 1LL << logm;
   const long long npairs = (batch + 1) / 2;
   const bool per = hs != 0;
-  // Filters: a complex signal per pair of outputs when filters differ; the
-  // two members of a pair use different filters then, so fall back to one
-  // signal per transform (imaginary part zero) in that case.
-  if (per) {
-    for (int b = 0; b < batch; b++) {
-      VS_TRY(run_fft_large(correlate, x + b * xs, xlen, 0, h + b * hs, hlen, 0,
-                           y + b * ys, ylen, 1, s));
-    }
-    return VS_OK;
-  }
+  // One filter for all signals (per-signal filters take the partitioned
+  // overlap-save path, vs_conv1d).
+  VS_REQUIRE(!per, "FFT convolution: per-signal filters need the overlap-save path");
   DeviceBuffer hz, z;
   VS_TRY(hz.alloc(M * sizeof(float2), s));
   VS_TRY(z.alloc(M * npairs * sizeof(float2), s));
@@ -605,6 +1021,92 @@ using namespace vs;
 
 extern "C" {
 
+#ifdef VS_CONV_STAMPS
+__attribute__((visibility("default"))) vs_status vs_conv_stamps(unsigned long long *out,
+                                                                 int n) {
+  VS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(conv::g_stamps),
+                             sizeof(unsigned long long) * std::min(n, conv::kStampMax) *
+                                 conv::kStampSlots));
+  return VS_OK;
+}
+
+__global__ __launch_bounds__(256) void lds_census_kernel(float *out) {
+  extern __shared__ float dyn[];
+  dyn[threadIdx.x] = threadIdx.x;
+  __syncthreads();
+  out[threadIdx.x] = dyn[255 - threadIdx.x];
+}
+
+__attribute__((visibility("default"))) float vs_residency_probe(int lds, int vg, int blocks,
+                                                                long long spin) {
+  float *out = nullptr;
+  (void)hipMalloc(&out, 1024);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  auto launch = [&] {
+    if (vg == 240)
+      hipLaunchKernelGGL(conv::residency_kernel<240>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
+    else if (vg == 168)
+      hipLaunchKernelGGL(conv::residency_kernel<168>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
+    else if (vg == 128)
+      hipLaunchKernelGGL(conv::residency_kernel<128>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
+    else
+      hipLaunchKernelGGL(conv::residency_kernel<0>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
+  };
+  launch();
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(e0, nullptr);
+  launch();
+  (void)hipEventRecord(e1, nullptr);
+  (void)hipEventSynchronize(e1);
+  float ms = -1;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipFree(out);
+  return ms;
+}
+
+// occupancy the runtime reports for a 256-thread kernel with `lds` bytes of
+// dynamic LDS (diagnostics)
+__attribute__((visibility("default"))) int vs_lds_occupancy(int lds) {
+  int n = -1;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &n, reinterpret_cast<const void *>(&lds_census_kernel), 256, lds);
+  return n;
+}
+
+// hipFuncGetAttributes of a real-block kernel: {numRegs, sharedSizeBytes,
+// localSizeBytes, maxThreadsPerBlock, binaryVersion} (diagnostics)
+__attribute__((visibility("default"))) int vs_conv_attrs(int which, int *out) {
+  hipFuncAttributes at{};
+  const void *f = which == 0
+                      ? reinterpret_cast<const void *>(&conv::real_conv_kernel<13, 32, true>)
+                      : reinterpret_cast<const void *>(&conv::residency_kernel<240>);
+  const hipError_t e = hipFuncGetAttributes(&at, f);
+  out[0] = at.numRegs;
+  out[1] = static_cast<int>(at.sharedSizeBytes);
+  out[2] = static_cast<int>(at.localSizeBytes);
+  out[3] = at.maxThreadsPerBlock;
+  out[4] = at.binaryVersion;
+  return e;
+}
+
+// occupancy the runtime reports for the real-block kernels (diagnostics)
+__attribute__((visibility("default"))) int vs_conv_occupancy(int which) {
+  int n = -1;
+  if (which == 0)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, reinterpret_cast<const void *>(&conv::real_conv_kernel<13, 32, true>), 256, 0);
+  else if (which == 1)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, reinterpret_cast<const void *>(&conv::real_conv_kernel<13, 16, true>), 512, 0);
+  else
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, reinterpret_cast<const void *>(&conv::real_conv_kernel<12, 0, true>), 256, 0);
+  return n;
+}
+#endif
+
 int vs_conv1d_select(int xlen, int hlen, int batch) {
   return conv::select(xlen, hlen, batch);
 }
@@ -620,6 +1122,15 @@ vs_status vs_tune_set(const char *key, int value) {
   }
   if (std::strcmp(key, "conv_buffer") == 0) {
     conv::g_conv_buf = value != 0;
+    return VS_OK;
+  }
+  if (std::strcmp(key, "conv_real") == 0) {
+    VS_REQUIRE(value >= 0 && value <= 2, "conv_real must be 0, 1 or 2");
+    conv::g_conv_real = value;
+    return VS_OK;
+  }
+  if (std::strcmp(key, "conv_real_all") == 0) {
+    conv::g_conv_real_all = value != 0;
     return VS_OK;
   }
   if (std::strcmp(key, "conv_split") == 0) {
@@ -643,30 +1154,40 @@ vs_status vs_conv1d(int algo, int correlate, const float *x, int xlen,
   if (batch == 0) return VS_OK;
   auto s = static_cast<hipStream_t>(stream);
   if (algo == VS_CONV_AUTO) algo = conv::select(xlen, hlen, batch);
-  if (batch > kMaxGridY && algo != VS_CONV_OVERLAP_SAVE)
+  if (batch > kMaxGridY)
     return batch_chunks(batch, [&](long long b0, int nb) {
       return vs_conv1d(algo, correlate, x + b0 * xs, xlen, xs, h + b0 * hs, hlen, hs,
                        y + b0 * ys, ys, nb, stream);
     });
   log(2, "vs_conv1d: x=%d h=%d batch=%d algo=%d", xlen, hlen, batch, algo);
+  int lm = 1;
+  while ((1LL << lm) < ylen) lm++;
   switch (algo) {
     case VS_CONV_DIRECT:
       return conv::run_direct(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
     case VS_CONV_OVERLAP_SAVE:
-      if ((1 << conv::os_block_log(hlen)) > hlen - 1 + 16)
-        return conv::run_block(correlate, true, x, xlen, xs, h, hlen, hs, y, ys,
-                               batch, s);
-      log(1, "vs_conv1d: filter %d too long for an overlap-save block, using FFT",
-          hlen);
-      [[fallthrough]];
-    case VS_CONV_FFT: {
-      int lm = 1;
-      while ((1LL << lm) < ylen) lm++;
-      if (lm <= fft::kMaxLdsLog)
-        return conv::run_block(correlate, false, x, xlen, xs, h, hlen, hs, y, ys,
-                               batch, s);
-      return conv::run_fft_large(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
-    }
+      if ((1 << conv::os_block_log(hlen)) > hlen - 1 + 16) {
+        if (conv::use_real(conv::os_block_log(hlen)))
+          return conv::run_real(correlate, true, x, xlen, xs, h, hlen, hs, y, ys,
+                                static_cast<int>(ylen), static_cast<int>(ylen), 0, batch, s);
+        return conv::run_block(correlate, true, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+      }
+      log(1, "vs_conv1d: filter %d longer than an overlap-save block: %d partitions", hlen,
+          (hlen + conv::kPartTaps - 1) / conv::kPartTaps);
+      return conv::run_partitioned(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+    case VS_CONV_FFT:
+      if (lm <= fft::kMaxLdsLog) {
+        if (conv::use_real(lm))
+          return conv::run_real(correlate, false, x, xlen, xs, h, hlen, hs, y, ys,
+                                static_cast<int>(ylen), static_cast<int>(ylen), 0, batch, s);
+        return conv::run_block(correlate, false, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+      }
+      if (lm <= fft::kMaxLog && hs == 0)
+        return conv::run_fft_large(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+      // beyond the largest transform, or one filter per signal: partitions
+      log(1, "vs_conv1d: FFT of 2^%d%s: partitioned overlap-save", lm,
+          hs ? " with per-signal filters" : "");
+      return conv::run_partitioned(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
   }
   set_error("vs_conv1d: unknown algorithm %d", algo);
   return VS_ERR_INVALID;

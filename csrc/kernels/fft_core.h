@@ -263,29 +263,30 @@ struct RegTw {
   }
 };
 
-// Compile-time pass plan for N = 2^LOGN, 16 points per thread (N >= 16).
-template <int LOGN_>
+// Compile-time pass plan for N = 2^LOGN.  EP = points per thread: 0 picks
+// the default (16, or 32 at N = 16384 so the 512-thread workgroup keeps its
+// working set in registers -- at 1024 threads the 128-VGPR budget of 4
+// waves/SIMD spilled); 32 runs radix-32 passes after one smaller first pass
+// (N = 16384: 16 x 32 x 32, N = 8192: 8 x 32 x 32) -- one butterfly of 32
+// per thread and a third fewer LDS round trips and barriers than radix 16.
+template <int LOGN_, int EP = 0>
 struct Plan {
   static constexpr int LOGN = LOGN_;
   static constexpr int N = 1 << LOGN;
-  // Points per thread: 16, or 32 at N = 16384 so the 512-thread workgroup
-  // keeps its working set in registers (at 1024 threads the 128-VGPR budget
-  // of 4 waves/SIMD spilled).
-  static constexpr int E = LOGN >= 14 ? 32 : (LOGN >= 4 ? 16 : N);
+  static constexpr int E = EP ? EP : (LOGN >= 14 ? 32 : (LOGN >= 4 ? 16 : N));
+  static_assert(E <= N && (E == 32 ? LOGN >= 6 : true), "plan: too few points");
   static constexpr int TPS = N / E;                // threads per signal
   static constexpr int SMALL = LOGN >= 4 ? LOGN % 4 : 0;
-  // N = 16384 runs 16 x 32 x 32 (3 passes, 2 LDS transposes) instead of
-  // 4 x 16 x 16 x 16: one butterfly of 32 per thread (E = 32) and a third
-  // fewer LDS round trips and barriers.
-  static constexpr bool R32 = LOGN == 14;
-  static constexpr int NPASS = R32 ? 3 : (LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1);
+  static constexpr bool R32 = E == 32;
+  static constexpr int NPASS =
+      R32 ? (LOGN + 4) / 5 : (LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1);
   // per-signal LDS (float2).  Signals narrower than a 32-lane read group
   // (TPS < 32, several per wave) are TPS slots apart so their aligned
   // TPS-slot read blocks land in different banks.
   static constexpr int kLds = N + (TPS < 32 ? TPS : 0);
   // Radix of pass q (forward order: the odd radix first).
   static constexpr int radix(int q) {
-    if (R32) return q == 0 ? 16 : 32;
+    if (R32) return q == 0 ? (1 << (LOGN - 5 * (NPASS - 1))) : 32;
     return LOGN < 4 ? N : ((SMALL && q == 0) ? (1 << SMALL) : 16);
   }
   static constexpr int radix_rev(int q) { return radix(NPASS - 1 - q); }

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One conv configuration a few times, for rocprofv3 kernel-trace / PMC runs.
-XLEN=1048576 HLEN=4096 BATCH=64 ALGO=0 REPS=5 [OSLOG=14]"""
+XLEN=1048576 HLEN=4096 BATCH=64 ALGO=0 REPS=5 [OSLOG=14] [CONV_REAL=0/1/2]"""
 import ctypes
 import os
 import sys
@@ -16,6 +16,9 @@ hl = int(os.environ.get("HLEN", 4096))
 batch = int(os.environ.get("BATCH", 64))
 algo = int(os.environ.get("ALGO", 0))
 reps = int(os.environ.get("REPS", 5))
+for knob in ("conv_real", "conv_buffer"):
+    if knob.upper() in os.environ:
+        lib.vs_tune_set(knob.encode(), int(os.environ[knob.upper()]))
 if "OSLOG" in os.environ:
     lib.vs_tune_set(b"os_block_log_max", int(os.environ["OSLOG"]))
 x = torch.randn(batch, xl, device="cuda")
