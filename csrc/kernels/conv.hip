@@ -634,56 +634,59 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS)) void real_conv_kernel(
 //   c = conj(a), d = conj(b)               (merge:  Z'[k] = c Y[k] + d Y*[M-k])
 //   P = (c a H[k] + d b H*[M-k]) / M,  Q = (c b H[k] + d a H*[M-k]) / M
 // with W = exp(-2 pi i / L) (k = 0 pairs with itself: H[M] is the Nyquist bin).
-template <int LOGM, int EP>
-__global__ __launch_bounds__((Plan<LOGM, EP>::TPS)) void real_filter_kernel(
+// One workgroup per filter, 16 points per thread whatever plan the block
+// kernel uses (a lone workgroup is latency-bound: more waves, and every
+// global load -- taps, both twiddle sets, the W^k of the split -- issued
+// before the first butterfly).
+template <int LOGM>
+__global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
     const float *__restrict__ h, int hlen, int64_t hs, int reverse,
     const float2 *__restrict__ tw, const float2 *__restrict__ twl, float4 *__restrict__ PQ) {
-  using PL = Plan<LOGM, EP>;
+  using PL = Plan<LOGM>;
+  constexpr int E = PL::E;
   __shared__ float2 lds[PL::N];
   const int t = threadIdx.x;
   const float *hr = h + static_cast<long long>(blockIdx.x) * hs;
   constexpr int R0 = PL::first_radix(false);
-  float2 v[PL::E];
-#pragma unroll
-  for (int b = 0; b < PL::E / R0; b++)
-#pragma unroll
-    for (int j = 0; j < R0; j++) {
-      const int n = 2 * reg_index<PL, R0>(t, b, j);
-      const float u0 = n < hlen ? hr[reverse ? hlen - 1 - n : n] : 0.f;
-      const float u1 = n + 1 < hlen ? hr[reverse ? hlen - 2 - n : n + 1] : 0.f;
-      v[b * R0 + j] = make_float2(u0, u1);
-    }
-  fft::transform<PL, false, false>(v, lds, t, tw);
   constexpr int RL = PL::last_radix(false);
+  float2 v[E], wk[E];
 #pragma unroll
-  for (int b = 0; b < PL::E / RL; b++)
+  for (int e = 0; e < E; e++) {
+    const int n = 2 * reg_index<PL, R0>(t, e / R0, e % R0);
+    const int i0 = reverse ? hlen - 1 - n : n, i1 = reverse ? hlen - 2 - n : n + 1;
+    const float u0 = hr[n < hlen ? i0 : 0], u1 = hr[n + 1 < hlen ? i1 : 0];
+    v[e] = make_float2(n < hlen ? u0 : 0.f, n + 1 < hlen ? u1 : 0.f);
+  }
 #pragma unroll
-    for (int j = 0; j < RL; j++)
-      lds[fft::lds_slot(reg_index<PL, RL>(t, b, j))] = v[b * RL + j];
+  for (int e = 0; e < E; e++) wk[e] = twl[reg_index<PL, RL>(t, e / RL, e % RL)];
+  fft::RegTw<PL, false> twf;
+  twf.load(t, tw);
+  __builtin_amdgcn_sched_barrier(0);
+  fft::transform<PL, false, false>(v, lds, t, twf);
+#pragma unroll
+  for (int e = 0; e < E; e++) lds[fft::lds_slot(reg_index<PL, RL>(t, e / RL, e % RL))] = v[e];
   fft::lds_barrier();
   float4 *out = PQ + static_cast<long long>(blockIdx.x) * PL::N;
   const float sc = 1.0f / static_cast<float>(PL::N);
 #pragma unroll
-  for (int b = 0; b < PL::E / RL; b++)
-#pragma unroll
-    for (int j = 0; j < RL; j++) {
-      const int k = reg_index<PL, RL>(t, b, j);
-      const float2 zk = v[b * RL + j];
-      const float2 zm = lds[fft::lds_slot((PL::N - k) & (PL::N - 1))];
-      const float2 w = twl[k];                   // W^k, W = exp(-2 pi i / L)
-      const float2 iw = make_float2(-w.y, w.x);  // i W^k
-      const float2 ca = make_float2(0.5f * (1.f - iw.x), -0.5f * iw.y);
-      const float2 cb = make_float2(0.5f * (1.f + iw.x), 0.5f * iw.y);
-      const float2 zmc = make_float2(zm.x, -zm.y);
-      const float2 hk = fft::cadd(cmul(ca, zk), cmul(cb, zmc));
-      // conj(H[M-k]) = a conj(Zh[M-k]) + b Zh[k]
-      const float2 hm = fft::cadd(cmul(ca, zmc), cmul(cb, zk));
-      const float2 cc = make_float2(ca.x, -ca.y);  // (1 + i W^-k)/2 = conj(a)
-      const float2 cd = make_float2(cb.x, -cb.y);  // (1 - i W^-k)/2 = conj(b)
-      const float2 P = fft::cadd(cmul(cmul(cc, ca), hk), cmul(cmul(cd, cb), hm));
-      const float2 Q = fft::cadd(cmul(cmul(cc, cb), hk), cmul(cmul(cd, ca), hm));
-      out[k] = make_float4(sc * P.x, sc * P.y, sc * Q.x, sc * Q.y);
-    }
+  for (int e = 0; e < E; e++) {
+    const int k = reg_index<PL, RL>(t, e / RL, e % RL);
+    const float2 zk = v[e];
+    const float2 zm = lds[fft::lds_slot((PL::N - k) & (PL::N - 1))];
+    const float2 w = wk[e];                    // W^k, W = exp(-2 pi i / L)
+    const float2 iw = make_float2(-w.y, w.x);  // i W^k
+    const float2 ca = make_float2(0.5f * (1.f - iw.x), -0.5f * iw.y);
+    const float2 cb = make_float2(0.5f * (1.f + iw.x), 0.5f * iw.y);
+    const float2 zmc = make_float2(zm.x, -zm.y);
+    const float2 hk = fft::cadd(cmul(ca, zk), cmul(cb, zmc));
+    // conj(H[M-k]) = a conj(Zh[M-k]) + b Zh[k]
+    const float2 hm = fft::cadd(cmul(ca, zmc), cmul(cb, zk));
+    const float2 cc = make_float2(ca.x, -ca.y);  // (1 + i W^-k)/2 = conj(a)
+    const float2 cd = make_float2(cb.x, -cb.y);  // (1 - i W^-k)/2 = conj(b)
+    const float2 P = fft::cadd(cmul(cmul(cc, ca), hk), cmul(cmul(cd, cb), hm));
+    const float2 Q = fft::cadd(cmul(cmul(cc, cb), hk), cmul(cmul(cd, ca), hm));
+    out[k] = make_float4(sc * P.x, sc * P.y, sc * Q.x, sc * Q.y);
+  }
 }
 
 template <int LOGM, int EP>
@@ -697,8 +700,9 @@ vs_status run_real_t(int correlate, const float *h, int hlen, int64_t hs, int nf
   if (!twl) return st;
   DeviceBuffer pq;
   VS_TRY(pq.alloc(sizeof(float4) * PL::N * static_cast<size_t>(nfilt), s));
-  hipLaunchKernelGGL((real_filter_kernel<LOGM, EP>), dim3(static_cast<unsigned>(nfilt)),
-                     dim3(PL::TPS), 0, s, h, hlen, hs, correlate, tw, twl, pq.as<float4>());
+  hipLaunchKernelGGL((real_filter_kernel<LOGM>), dim3(static_cast<unsigned>(nfilt)),
+                     dim3(Plan<LOGM>::TPS), 0, s, h, hlen, hs, correlate, tw, twl,
+                     pq.as<float4>());
   a.PQ = pq.as<float4>();
   const dim3 grid(static_cast<unsigned>(a.nblk), static_cast<unsigned>(nblocks / a.nblk));
   if (g_conv_buf && a.xlen < (1 << 29) && a.yroom < (1 << 29))

@@ -17,7 +17,7 @@ from veles.simd_amd import _lib  # noqa: E402
 
 lib = _lib.lib()
 lib.vs_tune_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
-DEFAULTS = {"conv_buffer": 1}
+DEFAULTS = {"conv_buffer": 1, "conv_real": 1, "conv_real_all": 0}
 
 
 def main():
