@@ -1,7 +1,10 @@
-// mathfun.h (reference inc/simd/mathfun.h:142-204): simd != 0 runs the
-// vs_math kernel, simd == 0 libm on the host.
+// mathfun.h (reference inc/simd/mathfun.h:142-204) and the array forms of
+// the avx_mathfun.h / neon_mathfun.h element functions (sincos, pow,
+// sqrt): simd != 0 runs the HIP kernels, simd == 0 libm on the host.
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include "simd/mathfun.h"
+#include "simd/avx_mathfun.h"
+#include "simd/neon_mathfun.h"
 
 #include "csrc/api/dispatch.h"
 #include "simd/gpu.h"
@@ -36,5 +39,43 @@ void log_psv(int simd, const float *src, size_t n, float *res) {
 }
 void exp_psv(int simd, const float *src, size_t n, float *res) {
   psv(simd, VS_FN_EXP, "exp_psv", expf, src, n, res);
+}
+void sqrt_psv(int simd, const float *src, size_t n, float *res) {
+  psv(simd, VS_FN_SQRT, "sqrt_psv", sqrtf, src, n, res);
+}
+
+void sincos_psv(int simd, const float *src, size_t n, float *s, float *c) {
+  if (!vs::api::use_gpu_simd(simd, "sincos_psv") || n == 0) {
+    sincos_psv_novec(src, n, s, c);
+    return;
+  }
+  vs::api::run_sync("sincos_psv", [&](hipStream_t st) {
+    vs::Staged os(s, n * 4, vs::Staged::kOut, st);
+    vs::Staged oc(c, n * 4, vs::Staged::kOut, st);
+    vs::Staged x(src, n * 4, vs::Staged::kIn, st);
+    VS_TRY(os.status());
+    VS_TRY(oc.status());
+    VS_TRY(x.status());
+    VS_TRY(vs_sincos(x.dev<float>(), os.dev<float>(), oc.dev<float>(), n, st));
+    VS_TRY(os.finish());
+    return oc.finish();
+  });
+}
+
+void pow_psv(int simd, const float *x, const float *y, size_t n, float *res) {
+  if (!vs::api::use_gpu_simd(simd, "pow_psv") || n == 0) {
+    pow_psv_novec(x, y, n, res);
+    return;
+  }
+  vs::api::run_sync("pow_psv", [&](hipStream_t st) {
+    vs::Staged o(res, n * 4, vs::Staged::kOut, st);
+    vs::Staged a(x, n * 4, vs::Staged::kIn, st);
+    vs::Staged b(y, n * 4, vs::Staged::kIn, st);
+    VS_TRY(o.status());
+    VS_TRY(a.status());
+    VS_TRY(b.status());
+    VS_TRY(vs_pow(a.dev<float>(), b.dev<float>(), o.dev<float>(), n, st));
+    return o.finish();
+  });
 }
 }  // extern "C"

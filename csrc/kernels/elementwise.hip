@@ -206,9 +206,48 @@ struct MathOp {
     if constexpr (FN == VS_FN_SIN) return sinf(x);
     if constexpr (FN == VS_FN_COS) return cosf(x);
     if constexpr (FN == VS_FN_LOG) return logf(x);
+    if constexpr (FN == VS_FN_SQRT) return sqrtf(x);  // correctly rounded
     return accurate_expf(x);
   }
 };
+// x^y evaluated in double and rounded once: OCML powf was measured at up
+// to 5 ulp (15.65^4.2); the double pow keeps every result within 1 ulp.
+// FP64 VALU runs at half the FP32 rate, which this HBM-bound map never
+// reaches (12 bytes per element).
+struct PowOp {
+  __device__ float operator()(float x, float y) const {
+    return static_cast<float>(pow(static_cast<double>(x), static_cast<double>(y)));
+  }
+};
+
+// sin and cos of the same argument: one shared range reduction per element
+// (OCML sincosf), two 16-byte stores per lane.
+__global__ __launch_bounds__(kBlock) void sincos_kernel(const float *__restrict__ x,
+                                                        float *__restrict__ s,
+                                                        float *__restrict__ c, size_t n) {
+  const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const size_t nv = n / 4;
+  for (size_t i = tid; i < nv; i += stride) {
+    const float4 v = reinterpret_cast<const float4 *>(x)[i];
+    float4 sv, cv;
+    sincosf(v.x, &sv.x, &cv.x);
+    sincosf(v.y, &sv.y, &cv.y);
+    sincosf(v.z, &sv.z, &cv.z);
+    sincosf(v.w, &sv.w, &cv.w);
+    reinterpret_cast<float4 *>(s)[i] = sv;
+    reinterpret_cast<float4 *>(c)[i] = cv;
+  }
+  for (size_t i = 4 * nv + tid; i < n; i += stride) sincosf(x[i], s + i, c + i);
+}
+
+__global__ __launch_bounds__(kBlock) void sincos_scalar_kernel(const float *__restrict__ x,
+                                                               float *__restrict__ s,
+                                                               float *__restrict__ c, size_t n) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    sincosf(x[i], s + i, c + i);
+}
 
 // ------------------------------------------------------- complex kernels
 // Two interleaved complex numbers per lane (one float4).
@@ -426,9 +465,31 @@ vs_status vs_math(int fn, const float *x, float *y, size_t n,
       return launch_map1(x, y, n, MathOp<VS_FN_LOG>{}, s);
     case VS_FN_EXP:
       return launch_map1(x, y, n, MathOp<VS_FN_EXP>{}, s);
+    case VS_FN_SQRT:
+      return launch_map1(x, y, n, MathOp<VS_FN_SQRT>{}, s);
   }
   set_error("vs_math: unknown function %d", fn);
   return VS_ERR_INVALID;
+}
+
+vs_status vs_pow(const float *x, const float *y, float *out, size_t n, vs_stream_t stream) {
+  VS_REQUIRE(x && y && out, "vs_pow: null pointer");
+  return launch_map2(x, y, out, n, PowOp{}, static_cast<hipStream_t>(stream));
+}
+
+vs_status vs_sincos(const float *x, float *s, float *c, size_t n, vs_stream_t stream) {
+  VS_REQUIRE(x && s && c, "vs_sincos: null pointer");
+  if (n == 0) return VS_OK;
+  auto st = static_cast<hipStream_t>(stream);
+  const auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (al(x) && al(s) && al(c))
+    hipLaunchKernelGGL(sincos_kernel, dim3(elementwise_grid((n + 3) / 4, kBlock)), dim3(kBlock),
+                       0, st, x, s, c, n);
+  else
+    hipLaunchKernelGGL(sincos_scalar_kernel, dim3(elementwise_grid(n, kBlock)), dim3(kBlock), 0,
+                       st, x, s, c, n);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
 }
 
 }  // extern "C"

@@ -67,7 +67,8 @@ typedef enum {
   VS_FN_SIN = 0,
   VS_FN_COS = 1,
   VS_FN_LOG = 2,
-  VS_FN_EXP = 3
+  VS_FN_EXP = 3,
+  VS_FN_SQRT = 4
 } vs_math_fn;
 
 /// dst[i] = convert(src[i]); float->int truncates, narrowing saturates.
@@ -96,6 +97,13 @@ vs_status vs_int16_multiply(const int16_t *a, const int16_t *b, int32_t *out,
                             size_t n, vs_stream_t stream);
 vs_status vs_math(int fn, const float *x, float *y, size_t n,
                   vs_stream_t stream);
+/// out[i] = powf(x[i], y[i]) (reference avx_mathfun.h:720 pow256_ps).
+vs_status vs_pow(const float *x, const float *y, float *out, size_t n,
+                 vs_stream_t stream);
+/// s[i] = sinf(x[i]), c[i] = cosf(x[i]) in one pass (reference
+/// avx_mathfun.h:571 sincos256_ps, neon_mathfun.h:228 sincos_ps).
+vs_status vs_sincos(const float *x, float *s, float *c, size_t n,
+                    vs_stream_t stream);
 
 /* ------------------------------------------------------------ reductions */
 /// *out_dev = sum(x) (pairwise tree in fp32).
@@ -126,18 +134,14 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
                                    int64_t ldc, int64_t stride_c, int batch,
                                    vs_stream_t stream);
 
-/// Tuning entry point: one explicit SGEMM tile variant (gen 1, k-major LDS:
-/// 0: 64x64x32, 1: 128x128x16, 2: 128x128x32, 3: 256x128x16, 4: 128x256x16;
-/// gen 2, k-contiguous LDS + interleaved schedule: 5: 128x128x32,
-/// 6: 256x128x32, 7: 128x256x32; NN whole-tile LDS-DMA kernels (other shapes
-/// fall back to gen 1/2): gen 3 8: 256x128x32, 9: 128x128x32, 10: 256x256x16,
-/// 11/12: the 16x16x4-MFMA forms of 8/9; gen 4, three-stage DMA ring:
-/// 13: 128x128, 14: 256x128, 15: 256x256 (BK 16); 16/17: 128x128 BK 32
-/// one wave per SIMD (asm / compiler fragment reads), 18: 256x128 BK 32;
-/// gen 5, hand-pipelined (barrier mid-tile, next tile's fragment reads
-/// interleaved with this tile's MFMAs): 19: 128x128 (2 blocks / CU),
-/// 20: 256x128 (waves of 128x64), 21: 128x128 (3 blocks / CU), 22: 256x256
-/// (waves of 128x128, AGPR accumulators), 23: variant 20 with AGPR accumulators).
+/// Number of SGEMM kernel variants accepted by vs_sgemm_variant.
+#define VS_SGEMM_VARIANTS 6
+/// Tuning entry point: one explicit SGEMM kernel variant.  Gen 6 (any
+/// transpose, ragged shapes, any alignment): 0: 64x64 tiles, 1: 128x128,
+/// 2: 256x256 (AGPR accumulators), 4: 64x64 with automatic split-K,
+/// 5: 128x128 with automatic split-K; 3: gen 5 256x256 for NN whole tiles
+/// (hand-pipelined LDS-DMA ring), gen 6 256x256 otherwise.  vs_sgemm picks
+/// 3 / 1 / 4 by output-tile count (csrc/kernels/sgemm.hip sgemm_impl).
 vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
                            int k, float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,

@@ -15,6 +15,10 @@
 #include <simd/attributes.h>
 #include <simd/common.h>
 #include <simd/instruction_set.h>
+/* sincos_psv / pow_psv / sqrt_psv: the reference's avx_mathfun.h /
+ * neon_mathfun.h element functions over arrays (reference mathfun.h
+ * includes those headers, :30-40). */
+#include <simd/neon_mathfun.h>
 
 SIMD_API_BEGIN
 

@@ -24,6 +24,10 @@ def pytest_configure(config):
 
 def pytest_collection_modifyitems(config, items):
     from veles.simd_amd import _lib
+    # A library that exists but does not load is a build error, never a
+    # reason to skip the GPU tests (they would pass as "skipped").
+    if os.path.exists(_lib.LIB_PATH) and not _lib.available():
+        raise pytest.UsageError(f"native library failed to load: {_lib._load_error}")
     if _lib.gpu_available():
         return
     skip = pytest.mark.skip(reason="no GPU visible to the native library")

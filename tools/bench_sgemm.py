@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """A/B the SGEMM tile variants in one process (interleaved rounds, median),
-against torch.matmul (hipBLASLt) on the same random data."""
+against torch.matmul (hipBLASLt, same transposes) on the same random data.
+SHAPES="MxNxK:tt,..." (tt = nn / nt / tn / tt), VARIANTS="0,1,2,3,4", ROUNDS,
+CHECK=0 skips the transpose check."""
 import ctypes
 import json
 import os
@@ -39,20 +41,35 @@ def check_transposes(variants):
     print("transpose check ok for variants", variants, flush=True)
 
 
+def parse_shapes(spec):
+    """"MxNxK:tt,..." with tt in nn / nt / tn / tt (A / B stored transposed)."""
+    out = []
+    for item in spec.split(","):
+        dims, _, tt = item.partition(":")
+        m, n, k = (int(v) for v in dims.split("x"))
+        tt = tt or "nn"
+        out.append((m, n, k, int(tt[0] == "t"), int(tt[1] == "t")))
+    return out
+
+
 def main():
-    shapes = [(4096, 4096, 4096), (8192, 8192, 8192), (2048, 2048, 2048),
-              (300, 1000, 256)]
+    shapes = parse_shapes(os.environ.get(
+        "SHAPES", "4096x4096x4096:nn,4096x4096x4096:nt,8192x8192x8192:nn,2048x2048x2048:nn,"
+                  "300x1000x256:nn,300x1000x256:nt,299x999x125:nn,299x999x125:nt"))
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4").split(",")]
     rounds = int(os.environ.get("ROUNDS", "5"))
-    check_transposes(variants)
+    if os.environ.get("CHECK", "1") == "1":
+        check_transposes(variants)
     torch.backends.cuda.matmul.allow_tf32 = False
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
-    for (m, n, k) in shapes:
-        a = torch.rand(m, k, device="cuda") * 2 - 1
-        b = torch.rand(k, n, device="cuda") * 2 - 1
+    for (m, n, k, ta, tb) in shapes:
+        a = torch.rand((k, m) if ta else (m, k), device="cuda") * 2 - 1
+        b = torch.rand((n, k) if tb else (k, n), device="cuda") * 2 - 1
+        ao = a.T if ta else a   # logical operands for torch (hipBLASLt transposes)
+        bo = b.T if tb else b
         c = torch.empty(m, n, device="cuda")
-        ref = a.double() @ b.double()
+        ref = ao.double() @ bo.double()
         reps = max(2, int(2e11 / (2 * m * n * k)))
         times = {v: [] for v in variants + ["torch"]}
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -60,10 +77,11 @@ def main():
             for v in variants + ["torch"]:
                 def run():
                     if v == "torch":
-                        torch.matmul(a, b, out=c)
+                        torch.matmul(ao, bo, out=c)
                     else:
-                        st = lib.vs_sgemm_variant(v, 0, 0, m, n, k, 1.0, a.data_ptr(), k,
-                                                  b.data_ptr(), n, 0.0, c.data_ptr(), n, s)
+                        st = lib.vs_sgemm_variant(v, ta, tb, m, n, k, 1.0, a.data_ptr(),
+                                                  a.shape[1], b.data_ptr(), b.shape[1], 0.0,
+                                                  c.data_ptr(), n, s)
                         assert st == 0, lib.vs_last_error()
                 run()
                 ev0.record()
@@ -77,9 +95,10 @@ def main():
                     assert err < 1e-5 * k + 1e-4, (v, err)
         out = {str(v): round(2 * m * n * k / statistics.median(t) / 1e9, 1)
                for v, t in times.items()}
-        res[f"{m}x{n}x{k}"] = out
-        print(f"{m}x{n}x{k} TFLOP/s (median of {rounds}):",
-              {kk: round(vv / 1e3, 1) for kk, vv in out.items()}, flush=True)
+        tag = f"{m}x{n}x{k}:{'tn'[ta == 0]}{'tn'[tb == 0]}"
+        res[tag] = out
+        print(f"{tag} TFLOP/s (median of {rounds}):",
+              out, flush=True)
     print(json.dumps(res))
 
 

@@ -4,7 +4,7 @@
 # Usage (from gpurun): bash tools/pmc_sgemm.sh VARIANTS SHAPE TAG
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-VARIANTS="${1:-15}"; SHAPE="${2:-4096}"; TAG="${3:-pmc}"
+VARIANTS="${1:-3}"; SHAPE="${2:-4096}"; TAG="${3:-pmc}"
 OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run each SGEMM variant (and torch.matmul) a few times at one shape, for
-rocprofv3 kernel-trace / PMC collection.  VARIANTS=1,4,5 SHAPE=4096 REPS=5."""
+rocprofv3 kernel-trace / PMC collection.  VARIANTS=2,3 SHAPE=4096 REPS=5."""
 import ctypes
 import os
 import sys
@@ -13,7 +13,7 @@ from veles.simd_amd import _lib  # noqa: E402
 lib = _lib.lib()
 n = int(os.environ.get("SHAPE", "4096"))
 reps = int(os.environ.get("REPS", "5"))
-variants = [int(v) for v in os.environ.get("VARIANTS", "1,4").split(",")]
+variants = [int(v) for v in os.environ.get("VARIANTS", "2,3").split(",")]
 torch.backends.cuda.matmul.allow_tf32 = False
 a = torch.rand(n, n, device="cuda") * 2 - 1
 b = torch.rand(n, n, device="cuda") * 2 - 1

@@ -80,6 +80,8 @@ _SIGNATURES = {
     "vs_conv1d_select": (_i, [_i, _i, _i]),
     "vs_conv1d_os_block": (_i, [_i]),
     "vs_tune_set": (_i, [ctypes.c_char_p, _i]),
+    "vs_pow": (_i, [_vp, _vp, _vp, _sz, _vp]),
+    "vs_sincos": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "vs_dwt": (_i, [_i, _i, _i, _vp, _i, _i64, _vp, _vp, _i64, _i, _vp]),
     "vs_swt": (_i, [_i, _i, _i, _i, _vp, _i, _i64, _vp, _vp, _i64, _i, _vp]),
     "vs_swt_multilevel": (_i, [_i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp]),

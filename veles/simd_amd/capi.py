@@ -59,6 +59,9 @@ _SIG = {
     "cos_psv": (None, [_i, _vp, _sz, _vp]),
     "log_psv": (None, [_i, _vp, _sz, _vp]),
     "exp_psv": (None, [_i, _vp, _sz, _vp]),
+    "sqrt_psv": (None, [_i, _vp, _sz, _vp]),
+    "sincos_psv": (None, [_i, _vp, _sz, _vp, _vp]),
+    "pow_psv": (None, [_i, _vp, _vp, _sz, _vp]),
     "normalize2D": (None, [_i, _vp, _i, _i, _i, _vp, _i]),
     "minmax2D": (None, [_i, _vp, _i, _i, _i, _vp, _vp]),
     "normalize2D_minmax": (None, [_i, ctypes.c_uint8, ctypes.c_uint8, _vp, _i,
@@ -173,6 +176,20 @@ def psv(name, simd, x):
     x = f32(x)
     res = np.empty_like(x)
     fn(name)(simd, p(x), x.size, p(res))
+    return res
+
+
+def sincos_psv(simd, x):
+    x = f32(x)
+    s, c = np.empty_like(x), np.empty_like(x)
+    fn("sincos_psv")(simd, p(x), x.size, p(s), p(c))
+    return s, c
+
+
+def pow_psv(simd, x, y):
+    x, y = f32(x), f32(y)
+    res = np.empty_like(x)
+    fn("pow_psv")(simd, p(x), p(y), x.size, p(res))
     return res
 
 

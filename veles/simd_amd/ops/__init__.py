@@ -9,7 +9,8 @@ from . import blas, elementwise, signal  # noqa: F401
 from .blas import gemm_bf16, matmul, matmul_transposed, sgemm, sgemm_bf16x3  # noqa: F401
 from .elementwise import (add, affine, binary, complex_conjugate,  # noqa: F401
                           complex_multiply, convert, cos, exp, log, math,
-                          minmax, mul, normalize2d, saxpy, sin, sub, sum_all)
+                          minmax, mul, normalize2d, pow, saxpy, sin, sincos, sqrt, sub,
+                          sum_all)
 from .signal import (conv1d, conv1d_algorithm, correlate, detect_peaks,  # noqa: F401
                      dwt, fft, irfft, rfft, swt, swt_level, wavedec,
                      wavelet_filter)

@@ -16,7 +16,7 @@ from ._util import on_device, ptr, require_gpu_tensor, stream_of
 VS_F32, VS_F16, VS_I16, VS_I32, VS_U8 = 0, 1, 2, 3, 4
 _DT = {torch.float32: VS_F32, torch.int16: VS_I16, torch.int32: VS_I32,
        torch.uint8: VS_U8, torch.float16: VS_F16}
-_FN = {"sin": 0, "cos": 1, "log": 2, "exp": 3}
+_FN = {"sin": 0, "cos": 1, "log": 2, "exp": 3, "sqrt": 4}
 _OP = {"add": 0, "sub": 1, "mul": 2}
 
 
@@ -204,6 +204,46 @@ def log(x):
 
 def exp(x):
     return math(x, "exp")
+
+
+def sqrt(x):
+    return math(x, "sqrt")
+
+
+@torch.library.custom_op("veles::pow", mutates_args=())
+def pow(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """x ** y elementwise (avx_mathfun.h pow256_ps over arrays)."""
+    if not _gpu(x, "veles::pow"):
+        return torch.pow(x, y)
+    x, y = torch.broadcast_tensors(x, y)
+    x, y = x.contiguous(), y.contiguous()
+    out = torch.empty_like(x)
+    with on_device(x):
+        _lib.call("vs_pow", ptr(x), ptr(y), ptr(out), x.numel(), stream_of(x))
+    return out
+
+
+@pow.register_fake
+def _(x, y):
+    return torch.empty(torch.broadcast_shapes(x.shape, y.shape), dtype=x.dtype,
+                       device=x.device)
+
+
+@torch.library.custom_op("veles::sincos", mutates_args=())
+def sincos(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """(sin x, cos x) in one pass (sincos256_ps / sincos_ps over arrays)."""
+    if not _gpu(x, "veles::sincos"):
+        return torch.sin(x), torch.cos(x)
+    x = x.contiguous()
+    s, c = torch.empty_like(x), torch.empty_like(x)
+    with on_device(x):
+        _lib.call("vs_sincos", ptr(x), ptr(s), ptr(c), x.numel(), stream_of(x))
+    return s, c
+
+
+@sincos.register_fake
+def _(x):
+    return torch.empty_like(x), torch.empty_like(x)
 
 
 # --------------------------------------------------------------- reductions
