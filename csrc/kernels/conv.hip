@@ -34,7 +34,7 @@
 
 namespace vs {
 namespace conv {
-extern int g_conv_buf, g_conv_split, g_conv_real, g_conv_real_all;  // tuning knobs, defined below
+extern int g_conv_buf, g_conv_real, g_conv_real_all;  // tuning knobs, defined below
 namespace {
 
 using fft::cmul;
@@ -335,15 +335,11 @@ __device__ __forceinline__ void store_pair(const BlockArgs &a, const PairPos &q,
 
 // One workgroup per block pair.  No barrier between the transforms: the
 // forward transform's last LDS read is followed by a barrier inside it.
-// SPLIT (16384 points): the LDS exchanges move real and imaginary parts one
-// after the other through a 68 KiB float image instead of a 137 KiB float2
-// one, so two workgroups share a CU (16 waves instead of 8, 128 VGPRs each)
-// and one's HBM loads / stores and barriers overlap the other's butterflies.
-template <int LOGN, bool BUF, bool SPLIT>
-__global__ __launch_bounds__(Plan<LOGN>::TPS, SPLIT ? 4 : 1) void block_conv_kernel(
+template <int LOGN, bool BUF>
+__global__ __launch_bounds__(Plan<LOGN>::TPS, 1) void block_conv_kernel(
     BlockArgs a, const float2 *__restrict__ tw) {
   using PL = Plan<LOGN>;
-  __shared__ std::conditional_t<SPLIT, float, float2> lds[PL::kLds];
+  __shared__ float2 lds[PL::kLds];
   const int t = threadIdx.x;
   const PairPos q = pair_pos(a, blockIdx.x);
   float2 v[PL::E];
@@ -352,11 +348,7 @@ __global__ __launch_bounds__(Plan<LOGN>::TPS, SPLIT ? 4 : 1) void block_conv_ker
   // scheduler otherwise splits them into dependent batches)
   __builtin_amdgcn_sched_barrier(0);
   fft::transform<PL, false, false>(v, lds, t, tw);
-  // SPLIT has half the registers: keep the spectrum loads from being
-  // hoisted into the forward transform (64 more live VGPRs)
-  if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);
   mul_spectrum<PL>(a, q, t, v);
-  if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);
   fft::transform<PL, true, true>(v, lds, t, tw);
   store_pair<PL, BUF>(a, q, t, v);
 }
@@ -366,23 +358,15 @@ inline bool buffer_ok(const BlockArgs &a) {
   return g_conv_buf && a.xlen < (1 << 29) && a.ylen < (1 << 29);
 }
 
-template <int LOGN, bool SPLIT>
-void launch_block_split(const BlockArgs &a, const float2 *tw, hipStream_t s) {
-  const unsigned grid = static_cast<unsigned>((a.nslots + 1) / 2);
-  if (buffer_ok(a))
-    hipLaunchKernelGGL((block_conv_kernel<LOGN, true, SPLIT>), dim3(grid),
-                       dim3(Plan<LOGN>::TPS), 0, s, a, tw);
-  else
-    hipLaunchKernelGGL((block_conv_kernel<LOGN, false, SPLIT>), dim3(grid),
-                       dim3(Plan<LOGN>::TPS), 0, s, a, tw);
-}
-
 template <int LOGN>
 void launch_block_t(const BlockArgs &a, const float2 *tw, hipStream_t s) {
-  if constexpr (LOGN == fft::kMaxLdsLog) {
-    if (g_conv_split) return launch_block_split<LOGN, true>(a, tw, s);
-  }
-  launch_block_split<LOGN, false>(a, tw, s);
+  const unsigned grid = static_cast<unsigned>((a.nslots + 1) / 2);
+  if (buffer_ok(a))
+    hipLaunchKernelGGL((block_conv_kernel<LOGN, true>), dim3(grid), dim3(Plan<LOGN>::TPS), 0, s,
+                       a, tw);
+  else
+    hipLaunchKernelGGL((block_conv_kernel<LOGN, false>), dim3(grid), dim3(Plan<LOGN>::TPS), 0, s,
+                       a, tw);
 }
 
 
@@ -767,9 +751,6 @@ int g_os_log_max = fft::kMaxLdsLog;
 // Tuning knob (vs_tune_set("conv_buffer", 0/1)): buffer-descriptor loads and
 // stores in the fused block kernels.
 int g_conv_buf = 1;
-// Tuning knob (vs_tune_set("conv_split", 0/1)): 16384-point block kernel with
-// the split (real, then imaginary) LDS exchange, two workgroups per CU.
-int g_conv_split = 0;
 // Tuning knob (vs_tune_set("conv_real", 0/1/2)): real-block kernel for the
 // overlap-save / single-block paths (0: pair kernel; 2: 16 points per thread
 // at M = 8192 instead of 32).
@@ -1135,10 +1116,6 @@ vs_status vs_tune_set(const char *key, int value) {
   }
   if (std::strcmp(key, "conv_real_all") == 0) {
     conv::g_conv_real_all = value != 0;
-    return VS_OK;
-  }
-  if (std::strcmp(key, "conv_split") == 0) {
-    conv::g_conv_split = value != 0;
     return VS_OK;
   }
   set_error("vs_tune_set: unknown key '%s'", key);

@@ -310,10 +310,7 @@ struct Pass {
   static constexpr int P = PL::stride(Q, REV);
   static constexpr int NB = PL::E / R;
 
-  // LT = float2: one exchange of the complex values through an N-point LDS
-  // image.  LT = float ("split"): the real parts, then the imaginary parts,
-  // through an N-float image -- half the LDS (two 16384-point workgroups per
-  // CU instead of one) for twice the barriers.
+  // One exchange of the complex values through an N-point LDS image.
   template <class TW, class LT>
   __device__ static void run(float2 (&v)[PL::E], LT *lds, int t, const TW &tw) {
 #pragma unroll
@@ -366,24 +363,10 @@ struct Pass {
           for (int j = 0; j < R2; j++) sink(b * R2 + j, lds[lds_slot(i + j * (PL::N / R2))]);
         }
       };
-      if constexpr (std::is_same_v<LT, float2>) {
-        put([](float2 z) { return z; });
-        lds_barrier();
-        get([&](int e, float2 z) { v[e] = z; });
-        lds_barrier();
-      } else {
-        // Once every real part is in LDS the registers' real halves are
-        // dead, so the new real parts land in them in place while the
-        // imaginary halves still hold the old ones: no temporary array.
-        put([](float2 z) { return z.x; });
-        lds_barrier();
-        get([&](int e, float z) { v[e].x = z; });
-        lds_barrier();
-        put([](float2 z) { return z.y; });
-        lds_barrier();
-        get([&](int e, float z) { v[e].y = z; });
-        lds_barrier();
-      }
+      put([](float2 z) { return z; });
+      lds_barrier();
+      get([&](int e, float2 z) { v[e] = z; });
+      lds_barrier();
       Pass<PL, INV, REV, Q + 1>::run(v, lds, t, tw);
     }
   }

@@ -12,14 +12,15 @@
 //
 // Structure: a prepass (split_kernel / pack_kernel) writes every operand as
 // a zero-padded, K-contiguous bf16 image ([Mp][Kp] for A, [Np][Kp] for B,
-// transposing B when it is stored [k][n]), so the main kernel has no edge
-// cases, only 16-byte loads and one layout.  Main kernel (template
-// <TERMS, BM, BN, WM, WN>, BK = 32): LDS images [rows][BK + 8] bf16 (80-byte
-// rows: the 16-lane groups of ds_read_b128 hit 16 distinct 4-bank groups),
-// two buffers, register-staged prefetch of tile t+1 during the MFMAs of tile
-// t, one barrier per k-tile; lane l of a 32x32x16 MFMA reads row l & 31,
-// k = 8 (l >> 5) .. +7 of both images with one ds_read_b128 each.  XCD-aware
-// grouped tile order as in sgemm.hip.
+// transposing B when it is stored [k][n]); a bf16 operand already stored
+// K-contiguous with whole tiles is read in place.  The main kernel
+// (gemm_glds_kernel) stages both images global -> LDS with
+// global_load_lds_dwordx4 into two XOR-swizzled stages and runs
+// v_mfma_f32_32x32x16_bf16 on 256 x 256 (bf16) / 256 x 128 (bf16x3) tiles,
+// or 128 x 128 tiles when the large ones cannot fill every CU.  (Round-1
+// register-staged, three/four-stage ring and transposed-read variants were
+// measured slower or spilled and are in git history,
+// profiles/r1/gemm_modes_v*.log.)
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include <hip/hip_runtime.h>
 
@@ -37,9 +38,6 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kBK = 32;   // k per LDS tile
-constexpr int kPad = 8;   // bf16 elements of row padding (16 bytes)
-constexpr int kP = kBK + kPad;
 
 __device__ __forceinline__ uint16_t bf16_bits(float x) {
   const __bf16 h = static_cast<__bf16>(x);
@@ -160,180 +158,6 @@ struct Args {
   int64_t ldc, sc;
 };
 
-template <int TERMS_, int BM_, int BN_, int WM_, int WN_>
-struct Cfg {
-  static constexpr int TERMS = TERMS_, BM = BM_, BN = BN_, WM = WM_, WN = WN_;
-  static constexpr int NIMG = TERMS == 1 ? 1 : 2;  // images per operand
-  static constexpr int kThreads = 64 * WM * WN;
-  static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  static constexpr int kImgA = BM * kP, kImgB = BN * kP;      // bf16 elements
-  static constexpr int kStage = NIMG * (kImgA + kImgB);
-  static constexpr int kLdsBytes = 2 * kStage * 2;
-  // 16-byte chunks per image per k-tile and per thread
-  static constexpr int kLoadsA = BM * kBK / 8 / kThreads;
-  static constexpr int kLoadsB = BN * kBK / 8 / kThreads;
-  static_assert(kLoadsA * 8 * kThreads == BM * kBK, "A tile split");
-  static_assert(kLoadsB * 8 * kThreads == BN * kBK, "B tile split");
-};
-
-template <int ROWS, int THREADS, int LOADS>
-struct Stage {
-  __device__ static void load(const uint16_t *__restrict__ img, int64_t ld, int row0,
-                              int k0, uint4 (&r)[LOADS]) {
-#pragma unroll
-    for (int l = 0; l < LOADS; l++) {
-      const int idx = threadIdx.x + l * THREADS;
-      const int row = idx / (kBK / 8), kc = (idx % (kBK / 8)) * 8;
-      r[l] = *reinterpret_cast<const uint4 *>(img + (row0 + row) * ld + k0 + kc);
-    }
-  }
-  __device__ static void store(uint16_t *__restrict__ s, const uint4 (&r)[LOADS]) {
-#pragma unroll
-    for (int l = 0; l < LOADS; l++) {
-      const int idx = threadIdx.x + l * THREADS;
-      const int row = idx / (kBK / 8), kc = (idx % (kBK / 8)) * 8;
-      *reinterpret_cast<uint4 *>(s + row * kP + kc) = r[l];
-    }
-  }
-};
-
-__device__ __forceinline__ bf16x8 frag(const uint16_t *s, int row, int k) {
-  return *reinterpret_cast<const bf16x8 *>(s + row * kP + k);
-}
-
-template <class C>
-__global__ __launch_bounds__(C::kThreads) void gemm_kernel(Args g) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  using SA = Stage<C::BM, C::kThreads, C::kLoadsA>;
-  using SB = Stage<C::BN, C::kThreads, C::kLoadsB>;
-  constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
-
-  const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
-  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
-  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  unsigned tm, tn;
-  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
-  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
-
-  const uint16_t *A[2], *B[2];
-#pragma unroll
-  for (int i = 0; i < NI; i++) {
-    A[i] = g.a[i] + blockIdx.z * g.sa;
-    B[i] = g.b[i] + blockIdx.z * g.sb;
-  }
-  float *Cp = g.c + blockIdx.z * g.sc;
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid / C::WN, wn = wid % C::WN;
-  const int lrow = lane & 31, lh = lane >> 5;
-  const int arow = wm * (C::BM / C::WM) + lrow;
-  const int brow = wn * (C::BN / C::WN) + lrow;
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; i++)
-#pragma unroll
-    for (int j = 0; j < TN; j++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-
-  uint4 ra[NI][C::kLoadsA], rb[NI][C::kLoadsB];
-  auto img_a = [&](int buf, int i) { return lds + buf * C::kStage + i * C::kImgA; };
-  auto img_b = [&](int buf, int i) {
-    return lds + buf * C::kStage + NI * C::kImgA + i * C::kImgB;
-  };
-  const int nk = g.kp / kBK;
-#pragma unroll
-  for (int i = 0; i < NI; i++) {
-    SA::load(A[i], g.lda, m0, 0, ra[i]);
-    SB::load(B[i], g.ldb, n0, 0, rb[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < NI; i++) {
-    SA::store(img_a(0, i), ra[i]);
-    SB::store(img_b(0, i), rb[i]);
-  }
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; kt++) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < NI; i++) {
-        SA::load(A[i], g.lda, m0, (kt + 1) * kBK, ra[i]);
-        SB::load(B[i], g.ldb, n0, (kt + 1) * kBK, rb[i]);
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < kBK / 16; ks++) {
-      const int ko = ks * 16 + 8 * lh;
-      bf16x8 fa[NI][TM], fb[NI][TN];
-#pragma unroll
-      for (int i = 0; i < NI; i++) {
-#pragma unroll
-        for (int x = 0; x < TM; x++) fa[i][x] = frag(img_a(cur, i), arow + 32 * x, ko);
-#pragma unroll
-        for (int y = 0; y < TN; y++) fb[i][y] = frag(img_b(cur, i), brow + 32 * y, ko);
-      }
-#pragma unroll
-      for (int x = 0; x < TM; x++)
-#pragma unroll
-        for (int y = 0; y < TN; y++) {
-          // small terms first, so the big one is added last
-          if (C::TERMS == 3) {
-            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][x], fb[0][y],
-                                                                acc[x][y], 0, 0, 0);
-            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[1][y],
-                                                                acc[x][y], 0, 0, 0);
-          }
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[0][y],
-                                                              acc[x][y], 0, 0, 0);
-        }
-    }
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < NI; i++) {
-        SA::store(img_a(cur ^ 1, i), ra[i]);
-        SB::store(img_b(cur ^ 1, i), rb[i]);
-      }
-    }
-    __syncthreads();
-  }
-
-  const bool use_beta = g.beta != 0.f;
-#pragma unroll
-  for (int x = 0; x < TM; x++)
-#pragma unroll
-    for (int y = 0; y < TN; y++) {
-      const int col = n0 + brow + 32 * y;
-      if (col >= g.n) continue;
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int row = m0 + arow - lrow + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row < g.m) {
-          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
-          float v = g.alpha * acc[x][y][r];
-          if (use_beta) v += g.beta * *pc;
-          *pc = v;
-        }
-      }
-    }
-}
-
-template <class C>
-vs_status launch(const Args &g, int batch, hipStream_t s) {
-  // per launch: the attribute is per device and the call is cheap
-  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_kernel<C>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes));
-  const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
-                                               ((g.n + C::BN - 1) / C::BN));
-  hipLaunchKernelGGL(gemm_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
-                     dim3(C::kThreads), C::kLdsBytes, s, g);
-  VS_HIP(hipGetLastError());
-  return VS_OK;
-}
-
 // Pack one operand.  rows x cols is the logical op(X) with rows along the
 // output (M or N) and cols along K; `trans` = element (r, c) at src[c*ld + r].
 vs_status pack(bool split, bool trans, const void *src, int64_t ld, int rows, int cols,
@@ -422,52 +246,7 @@ __device__ __forceinline__ bf16x8 gfrag(const uint8_t *img, int row, int c) {
   return *reinterpret_cast<const bf16x8 *>(img + row * C::RB + swz<C>(row, c) * 16);
 }
 
-// B read in place from its [K][N] storage (the NN layout, no transposing
-// prepass): the LDS image is [BK][BN] bf16 (k rows of BN * 2 bytes) filled
-// by the same lane-linear DMA, 16-byte chunk c of row k stored at chunk
-// c ^ ((k & 3) << 2), and the 32x32x16 B operand comes out of it
-// column-major through ds_read_b64_tr_b16 (cdna_hip_programming.md T10):
-// 16-lane group g (k rows 8 (g >> 1) + 0..3, then + 4..7, columns
-// 16 (g & 1) + 0..15), lane 4q + p addressing row q, columns 4p .. 4p + 3.
-// With the XOR each 32-lane half's 4 rows x 2 column blocks cover 64
-// distinct banks.
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-
 template <class C>
-__device__ __forceinline__ void dma_image_kn(const uint16_t *__restrict__ img, int64_t ld,
-                                             int col0, int k0, uint8_t *dst, int wave,
-                                             int lane) {
-  constexpr int RB = C::BN * 2, NCB = C::BN / 8, RPI = 1024 / RB;
-  static_assert(RB <= 1024 && 1024 % RB == 0 && NCB >= 16, "BN for the [K][N] image");
-#pragma unroll
-  for (int i = 0; i < C::kInstrB; i++) {
-    const int j = wave * C::kInstrB + i;
-    const int row = j * RPI + lane / NCB;
-    const int c = (lane % NCB) ^ ((row & 3) << 2);
-    const uint16_t *src = img + static_cast<int64_t>(k0 + row) * ld + col0 + 8 * c;
-    __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(dst + j * 1024), 16, 0,
-                                     0);
-  }
-}
-
-template <class C>
-__device__ __forceinline__ bf16x8 tr_frag(const uint8_t *img, int col0, int kb, int lane) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int col = col0 + 16 * (g & 1) + 4 * p;
-  const int k = kb + 8 * (g >> 1) + q;
-  const auto at = [&](int kr) {
-    return (lds_v4i16 *)(img + kr * (C::BN * 2) + (((col >> 3) ^ ((kr & 3) << 2)) << 4) +
-                         (col & 7) * 2);
-  };
-  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(at(k));
-  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(at(k + 4));
-  typedef short v8i16 __attribute__((ext_vector_type(8)));
-  const v8i16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, r);
-}
-
-template <class C, bool BKN = false>
 __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
   extern __shared__ __attribute__((aligned(1024))) uint8_t glds_lds[];
   constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
@@ -498,8 +277,7 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
 #pragma unroll
     for (int i = 0; i < NI; i++) {
       dma_image<C, C::kInstrA>(A[i], g.lda, m0, k0, img_a(buf, i), wid, lane);
-      if constexpr (BKN) dma_image_kn<C>(B[i], g.ldb, n0, k0, img_b(buf, i), wid, lane);
-      else dma_image<C, C::kInstrB>(B[i], g.ldb, n0, k0, img_b(buf, i), wid, lane);
+      dma_image<C, C::kInstrB>(B[i], g.ldb, n0, k0, img_b(buf, i), wid, lane);
     }
   };
 
@@ -527,12 +305,7 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
 #pragma unroll
         for (int x = 0; x < TM; x++) fa[i][x] = gfrag<C>(img_a(cur, i), arow + 32 * x, c);
 #pragma unroll
-        for (int y = 0; y < TN; y++) {
-          if constexpr (BKN)
-            fb[i][y] = tr_frag<C>(img_b(cur, i), brow - lrow + 32 * y, 16 * ks, lane);
-          else
-            fb[i][y] = gfrag<C>(img_b(cur, i), brow + 32 * y, c);
-        }
+        for (int y = 0; y < TN; y++) fb[i][y] = gfrag<C>(img_b(cur, i), brow + 32 * y, c);
       }
 #pragma unroll
       for (int x = 0; x < TM; x++)
@@ -572,180 +345,22 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     }
 }
 
-template <class C, bool BKN = false>
+template <class C>
 vs_status launch_glds(const Args &g, int batch, hipStream_t s) {
-  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_glds_kernel<C, BKN>),
+  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_glds_kernel<C>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes));
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
-  hipLaunchKernelGGL((gemm_glds_kernel<C, BKN>), dim3(tiles, 1, static_cast<unsigned>(batch)),
+  hipLaunchKernelGGL((gemm_glds_kernel<C>), dim3(tiles, 1, static_cast<unsigned>(batch)),
                      dim3(C::kThreads), C::kLdsBytes, s, g);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
 
-// Three-stage LDS-DMA ring (as SGEMM generation 4, sgemm.hip): the DMA of
-// tile t+2 stays in flight across tile t's raw barrier; one __shared__ array
-// per stage and the k loop unrolled by three so the compiler can tell the
-// in-flight DMA from the stage being read (no vmcnt(0) drain); counted waits
-// through __builtin_amdgcn_s_waitcnt.
-template <int N>
-__device__ __forceinline__ void bf_wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 0xF) | ((N >> 4) << 14));
-}
-
-// NS = 4 (BK = 32 images, 4 x 32 KiB): two tiles' DMA stay in flight
-// across each barrier instead of one -- more bytes in flight per CU against
-// the L2 / HBM latency, which the PMC wait fraction of the two-stage kernel
-// (39 % of wave cycles waiting, no LDS bank conflicts) points at.
-template <class C, int NS>
-__global__ __launch_bounds__(C::kThreads) void gemm_ring_kernel(Args g) {
-  static_assert(NS == 3 || NS == 4, "ring depth");
-  __shared__ __attribute__((aligned(1024))) uint8_t r0[C::kStage];
-  __shared__ __attribute__((aligned(1024))) uint8_t r1[C::kStage];
-  __shared__ __attribute__((aligned(1024))) uint8_t r2[C::kStage];
-  __shared__ __attribute__((aligned(1024))) uint8_t r3[NS == 4 ? C::kStage : 1];
-  constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
-  constexpr int kInstr = NI * (C::kInstrA + C::kInstrB);  // DMA per wave per tile
-  const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
-  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
-  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  unsigned tm, tn;
-  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
-  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
-  const uint16_t *A[2], *B[2];
-#pragma unroll
-  for (int i = 0; i < NI; i++) {
-    A[i] = g.a[i] + blockIdx.z * g.sa;
-    B[i] = g.b[i] + blockIdx.z * g.sb;
-  }
-  float *Cp = g.c + blockIdx.z * g.sc;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid / C::WN, wn = wid % C::WN;
-  const int lrow = lane & 31, lh = lane >> 5;
-  const int arow = wm * (C::BM / C::WM) + lrow;
-  const int brow = wn * (C::BN / C::WN) + lrow;
-
-  auto stage = [&](uint8_t *base, int k0) {
-#pragma unroll
-    for (int i = 0; i < NI; i++) {
-      dma_image<C, C::kInstrA>(A[i], g.lda, m0, k0, base + i * C::kImgA, wid, lane);
-      dma_image<C, C::kInstrB>(B[i], g.ldb, n0, k0, base + NI * C::kImgA + i * C::kImgB,
-                               wid, lane);
-    }
-  };
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; i++)
-#pragma unroll
-    for (int j = 0; j < TN; j++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-
-  auto compute = [&](const uint8_t *base) {
-#pragma unroll
-    for (int ks = 0; ks < C::BK / 16; ks++) {
-      const int c = 2 * ks + lh;
-      bf16x8 fa[NI][TM], fb[NI][TN];
-#pragma unroll
-      for (int i = 0; i < NI; i++) {
-#pragma unroll
-        for (int x = 0; x < TM; x++)
-          fa[i][x] = gfrag<C>(base + i * C::kImgA, arow + 32 * x, c);
-#pragma unroll
-        for (int y = 0; y < TN; y++)
-          fb[i][y] = gfrag<C>(base + NI * C::kImgA + i * C::kImgB, brow + 32 * y, c);
-      }
-#pragma unroll
-      for (int x = 0; x < TM; x++)
-#pragma unroll
-        for (int y = 0; y < TN; y++) {
-          if (C::TERMS == 3) {
-            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][x], fb[0][y],
-                                                                acc[x][y], 0, 0, 0);
-            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[1][y],
-                                                                acc[x][y], 0, 0, 0);
-          }
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][x], fb[0][y],
-                                                              acc[x][y], 0, 0, 0);
-        }
-    }
-  };
-
-  const int nk = g.kp / C::BK;
-  stage(r0, 0);
-  if (nk > 1) stage(r1, C::BK);
-  if (NS == 4 && nk > 2) stage(r2, 2 * C::BK);
-  // tile kt's DMA has landed once at most the later tiles' DMA (kt+1 ..
-  // kt+NS-2, those that exist) are outstanding
-#define VS_RING_STEP(CUR, NEXT)                              \
-  if (kt < nk) {                                             \
-    if (NS == 4 && kt + 2 < nk) bf_wait_vmcnt<2 * kInstr>(); \
-    else if (kt + 1 < nk) bf_wait_vmcnt<kInstr>();           \
-    else bf_wait_vmcnt<0>();                                 \
-    __builtin_amdgcn_s_barrier();                            \
-    if (kt + NS - 1 < nk) stage(NEXT, (kt + NS - 1) * C::BK); \
-    compute(CUR);                                            \
-  }                                                          \
-  kt++;
-  if constexpr (NS == 3) {
-    for (int kt = 0; kt < nk;) {
-      VS_RING_STEP(r0, r2)
-      VS_RING_STEP(r1, r0)
-      VS_RING_STEP(r2, r1)
-    }
-  } else {
-    for (int kt = 0; kt < nk;) {
-      VS_RING_STEP(r0, r3)
-      VS_RING_STEP(r1, r0)
-      VS_RING_STEP(r2, r1)
-      VS_RING_STEP(r3, r2)
-    }
-  }
-#undef VS_RING_STEP
-
-  const bool use_beta = g.beta != 0.f;
-#pragma unroll
-  for (int x = 0; x < TM; x++)
-#pragma unroll
-    for (int y = 0; y < TN; y++) {
-      const int col = n0 + brow + 32 * y;
-      if (col >= g.n) continue;
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int row = m0 + arow - lrow + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row < g.m) {
-          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
-          float v = g.alpha * acc[x][y][r];
-          if (use_beta) v += g.beta * *pc;
-          *pc = v;
-        }
-      }
-    }
-}
-
-template <class C, int NS = 3>
-vs_status launch_ring(const Args &g, int batch, hipStream_t s) {
-  const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
-                                               ((g.n + C::BN - 1) / C::BN));
-  hipLaunchKernelGGL((gemm_ring_kernel<C, NS>), dim3(tiles, 1, static_cast<unsigned>(batch)),
-                     dim3(C::kThreads), 0, s, g);
-  VS_HIP(hipGetLastError());
-  return VS_OK;
-}
-
-using R1 = GCfg<1, 256, 128, 64, 4, 2>;   // bf16: 3 x 48 KiB stages, 8 waves of 64 x 64
-using R1S = GCfg<1, 256, 256, 32, 2, 4>;  // bf16: 3 x 32 KiB stages, 8 waves of 128 x 64
-using R3 = GCfg<3, 256, 128, 32, 4, 2>;   // bf16x3: 3 x 48 KiB stages
-
 using G1 = GCfg<1, 256, 256, 64, 2, 4>;   // bf16: 128 KiB LDS, 8 waves of 128 x 64
 using G3 = GCfg<3, 256, 128, 32, 4, 2>;   // bf16x3: 96 KiB LDS, 8 waves of 64 x 64
-
-using C3 = Cfg<3, 128, 128, 2, 2>;
-using C3L = Cfg<3, 256, 128, 4, 2>;
-using C1 = Cfg<1, 128, 128, 2, 2>;
-using C1L = Cfg<1, 256, 128, 4, 2>;
+using G1S = GCfg<1, 128, 128, 64, 2, 2>;  // bf16, small problems: 64 KiB, 4 waves of 64 x 64
+using G3S = GCfg<3, 128, 128, 32, 2, 2>;  // bf16x3, small problems: 64 KiB
 
 int env_variant() {
   static const int v = [] {
@@ -775,26 +390,15 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   }
   if (variant < 0) variant = env_variant();
   if (variant < 0) {
-    const long t256 = static_cast<long>((m + 255) / 256) * ((n + 127) / 128) * batch;
-    variant = t256 >= 256 ? 2 : (t256 >= 128 ? 1 : 0);
+    // large tiles once they fill every CU, else 128 x 128
+    const long tl = static_cast<long>((m + G1::BM - 1) / G1::BM) * ((n + G1::BN - 1) / G1::BN) *
+                    batch;
+    variant = tl >= 256 ? 1 : 0;
   }
-  VS_REQUIRE(variant >= 0 && variant <= 6, "gemm_bf16: unknown variant %d", variant);
-  const bool tr_variant = variant == 6;
-  if (tr_variant) variant = 2;
-  int bm = variant == 1 ? 256 : 128, bn = 128, bk = kBK;
-  if (variant == 2) {
-    bm = split ? G3::BM : G1::BM;
-    bn = split ? G3::BN : G1::BN;
-    bk = split ? G3::BK : G1::BK;
-  } else if (variant == 3 || (variant >= 4 && split)) {
-    bm = split ? R3::BM : R1::BM;
-    bn = split ? R3::BN : R1::BN;
-    bk = split ? R3::BK : R1::BK;
-  } else if (variant >= 4) {
-    bm = R1S::BM;
-    bn = R1S::BN;
-    bk = R1S::BK;
-  }
+  VS_REQUIRE(variant == 0 || variant == 1, "gemm_bf16: unknown variant %d (0, 1)", variant);
+  const int bm = variant == 1 ? (split ? G3::BM : G1::BM) : (split ? G3S::BM : G1S::BM);
+  const int bn = variant == 1 ? (split ? G3::BN : G1::BN) : (split ? G3S::BN : G1S::BN);
+  const int bk = variant == 1 ? (split ? G3::BK : G1::BK) : (split ? G3S::BK : G1S::BK);
   const int mp = (m + bm - 1) / bm * bm, np = (n + bn - 1) / bn * bn;
   const int kp = k == 0 ? bk : (k + bk - 1) / bk * bk;
   const int ni = split ? 2 : 1;
@@ -811,13 +415,7 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
            (batch == 1 || st % 8 == 0) && reinterpret_cast<uintptr_t>(p) % 16 == 0;
   };
   const bool da = direct(ta == 0, m, mp, a, lda, sa);
-  // Variant 6: the two-stage LDS-DMA kernel with B read in place from [K][N]
-  // storage (tr-read image), i.e. NN without the transposing prepass.
-  // Measured slower than prepass + row reads (4096^3: 915 vs 933 TF, 8192^3:
-  // 983 vs 1108, profiles/r1/gemm_modes_v7_trread.log), so auto keeps the
-  // prepass; falls back to variant 2 when B is not a whole-tile [K][N] image.
-  const bool dbkn = tr_variant && direct(tb == 0, n, np, b, ldb, sb);
-  const bool db = dbkn || direct(tb != 0, n, np, b, ldb, sb);
+  const bool db = direct(tb != 0, n, np, b, ldb, sb);
   const size_t ea = static_cast<size_t>(mp) * kp, eb = static_cast<size_t>(np) * kp;
   const size_t wa = da ? 0 : ea * ni * batch, wb = db ? 0 : eb * ni * batch;
   DeviceBuffer buf;
@@ -859,14 +457,8 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   g.c = c;
   g.ldc = ldc;
   g.sc = sc;
-  if (dbkn) return launch_glds<G1, true>(g, batch, s);
-  if (variant == 2) return split ? launch_glds<G3>(g, batch, s) : launch_glds<G1>(g, batch, s);
-  if (variant == 3 || (variant >= 4 && split))
-    return split ? launch_ring<R3>(g, batch, s) : launch_ring<R1>(g, batch, s);
-  if (variant == 4) return launch_ring<R1S>(g, batch, s);
-  if (variant == 5) return launch_ring<R1S, 4>(g, batch, s);
-  if (split) return variant == 1 ? launch<C3L>(g, batch, s) : launch<C3>(g, batch, s);
-  return variant == 1 ? launch<C1L>(g, batch, s) : launch<C1>(g, batch, s);
+  if (variant == 1) return split ? launch_glds<G3>(g, batch, s) : launch_glds<G1>(g, batch, s);
+  return split ? launch_glds<G3S>(g, batch, s) : launch_glds<G1S>(g, batch, s);
 }
 
 }  // namespace

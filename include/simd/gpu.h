@@ -153,11 +153,8 @@ vs_status vs_gemm_bf16(int trans_a, int trans_b, int m, int n, int k,
                        float alpha, const uint16_t *a, int64_t lda,
                        const uint16_t *b, int64_t ldb, float beta, float *c,
                        int64_t ldc, vs_stream_t stream);
-/// Tuning entry point: explicit bf16 kernel variant (0: 128x128, 1: 256x128
-/// register-staged; 2: LDS-DMA 256x256 two-stage; 3: LDS-DMA three-stage
-/// ring 256x128 BK 64; 4: ring 256x256 BK 32; 5: four-stage ring 256x256
-/// BK 32; 6: variant 2 reading a [K][N] B in place through ds_read_b64_tr_b16;
-/// -1 auto).
+/// Tuning entry point: explicit bf16 kernel variant (LDS-DMA two-stage;
+/// 0: 128x128 tiles, 1: 256x256 (bf16) / 256x128 (bf16x3); -1 auto).
 vs_status vs_gemm_bf16_variant(int variant, int trans_a, int trans_b, int m, int n,
                                int k, float alpha, const uint16_t *a, int64_t lda,
                                const uint16_t *b, int64_t ldb, float beta, float *c,
