@@ -7,7 +7,10 @@ SGEMM (C = A @ B, MFMA f32 kernel) per GPU; `value` is the whole-job
 aggregate GFLOP/s (weak scaling: every rank multiplies its own pair of
 matrices).  The second half of the metric, 1D convolution throughput at
 signal length 2^20 (filter 4096, batch 64 per GPU, auto-selected algorithm),
-is timed the same way and reported in `secondary`.
+is timed the same way and reported in `secondary`, as are two
+communication-bearing BASELINE configurations: row-split batched SGEMM
+8192^2 (C row blocks all-gathered over RCCL / xGMI, config 5) and the SWT
+db8 x 8 levels over 65536 signals sharded data-parallel (config 4).
 
 Run: python bench.py --gpus N --steps K --warmup W   (N > 1 under
 torch.distributed.run; one rank per GPU, RCCL backend).
@@ -71,6 +74,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-conv", action="store_true")
+    ap.add_argument("--no-comm", action="store_true",
+                    help="skip the row-split SGEMM / SWT data-parallel secondaries")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -157,6 +162,64 @@ def main():
                               "algorithm": ["direct", "fft", "overlap_save"][
                                   max(0, algo - 1)]},
         })
+
+    # ------------------------------------- comm-bearing BASELINE configs
+    # Config 5 (row-split batched SGEMM 8192^2, RCCL all-gather of the C row
+    # blocks over xGMI, overlapped with the next matrix's GEMM; batch 8 of
+    # the config's 64 to stay within the bench's time budget) and config 4
+    # (SWT db8 x 8 levels over 65536 x 1024 signals, batch sharded over the
+    # ranks).  Both run under the same barrier / max-over-ranks clock.
+    if not args.no_comm:
+        from veles.simd_amd import parallel
+        rs_n, rs_batch = 8192, 8
+        m_loc = rs_n // world
+        ga = torch.Generator(device="cuda").manual_seed(77 + rank)
+        a_loc = torch.rand(rs_batch, m_loc, rs_n, device="cuda", generator=ga) - 0.5
+        bmat = torch.rand(rs_batch, rs_n, rs_n, device="cuda",
+                          generator=torch.Generator(device="cuda").manual_seed(99)) - 0.5
+        cfull = torch.empty(rs_batch, m_loc * world, rs_n, device="cuda")
+        rsteps = max(2, args.steps // 10)
+        dtr = _timed(lambda: parallel.rowsplit_bmm(a_loc, bmat, out=cfull), rsteps, 1, dist_on)
+        # numerics: this rank's rows of the first matrix, 64 rows
+        r0 = rank * m_loc
+        got = cfull[0, r0:r0 + 64].double()
+        ref = a_loc[0, :64].double() @ bmat[0].double()
+        rs_err = (got - ref).abs().max().item()
+        if rs_err > 2e-6 * rs_n:
+            raise RuntimeError(f"row-split SGEMM numerics check failed: {rs_err}")
+        secondary.update({
+            "rowsplit_sgemm_gflops": round(2.0 * rs_n ** 3 * rs_batch * rsteps / dtr / 1e9, 1),
+            "rowsplit_ms_per_step": round(dtr / rsteps * 1e3, 2),
+            "rowsplit_allgather_GB_per_rank_per_step": round(
+                rs_batch * (world - 1) * m_loc * rs_n * 4 / 1e9, 3),
+            "rowsplit_config": {"n": rs_n, "batch": rs_batch, "parallelism": f"tp{world}",
+                                "collective": "all_gather_into_tensor (RCCL)" if world > 1
+                                else "none (1 rank)"},
+        })
+        del a_loc, bmat, cfull
+
+        total, sn, levels = 65536, 1024, 8
+        s0, s1 = parallel.shard_range(total, world, rank)
+        xs = torch.randn(s1 - s0, sn, device="cuda", generator=ga)
+        hi = torch.empty(s1 - s0, levels, sn, device="cuda")
+        lo = torch.empty(s1 - s0, sn, device="cuda")
+
+        def swt_step():
+            st = lib.vs_swt_multilevel(0, 8, levels, 0, ctypes.c_void_p(xs.data_ptr()), sn,
+                                       ctypes.c_void_p(hi.data_ptr()),
+                                       ctypes.c_void_p(lo.data_ptr()), s1 - s0, stream)
+            if st:
+                raise RuntimeError(lib.vs_last_error().decode())
+
+        ssteps = max(5, args.steps // 2)
+        dts = _timed(swt_step, ssteps, 2, dist_on)
+        secondary.update({
+            "swt_dp_msamples_per_s": round(total * sn * ssteps / dts / 1e6, 1),
+            "swt_dp_ms_per_step": round(dts / ssteps * 1e3, 3),
+            "swt_dp_config": {"wavelet": "db8", "levels": levels, "signals": total,
+                              "len": sn, "parallelism": f"dp{world}"},
+        })
+        del xs, hi, lo
 
     base = _baseline()
     vs_base = None

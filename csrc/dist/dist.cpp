@@ -169,6 +169,39 @@ vs_status all_gather_on(vs_dist_context *c, const std::vector<hipStream_t> &s,
   return local_fence(c, s);
 }
 
+// Variable-size all-gather in place: rank q's block of bytes[q] at offset
+// off[q] of its buffer bufs[q] lands at the same offset of every rank's
+// buffer.  RCCL: one group of in-place broadcasts, one per root (RCCL has
+// no all-gatherv); over xGMI every root reaches every rank in one hop.
+vs_status all_gatherv_on(vs_dist_context *c, const std::vector<hipStream_t> &s,
+                         void *const *bufs, const size_t *off, const size_t *bytes) {
+  if (c->backend == VS_DIST_RCCL) {
+    VS_NCCL(ncclGroupStart());
+    for (int q = 0; q < c->n; q++) {
+      if (bytes[q] == 0) continue;
+      for (int r = 0; r < c->n; r++) {
+        DevGuard g(c->dev[r]);
+        char *p = static_cast<char *>(bufs[r]) + off[q];
+        VS_NCCL(ncclBroadcast(p, p, bytes[q], ncclChar, q, c->comms[r], s[r]));
+      }
+    }
+    VS_NCCL(ncclGroupEnd());
+    return VS_OK;
+  }
+  Events ready(c);
+  VS_TRY(ready.record(s));
+  for (int r = 0; r < c->n; r++) {
+    DevGuard g(c->dev[r]);
+    for (int q = 0; q < c->n; q++) {
+      if (q == r || bytes[q] == 0) continue;
+      VS_TRY(ready.wait(s[r], q));
+      VS_TRY(copy(c, static_cast<char *>(bufs[r]) + off[q], r,
+                  static_cast<const char *>(bufs[q]) + off[q], q, bytes[q], s[r]));
+    }
+  }
+  return local_fence(c, s);
+}
+
 vs_status halo_on(vs_dist_context *c, const std::vector<hipStream_t> &s,
                   const float *const *src, const size_t *len, float *const *halo,
                   size_t h, int direction, int periodic) {
@@ -485,62 +518,112 @@ vs_status vs_dist_sgemm_rowsplit(vs_dist_t c, int m, int n, int k, const float *
   VS_REQUIRE(A && B && C, "vs_dist_sgemm_rowsplit: null pointer");
   VS_REQUIRE(m > 0 && n > 0 && k > 0 && batch > 0, "vs_dist_sgemm_rowsplit: bad shape");
   const int R = c->n;
-  const size_t pad = (static_cast<size_t>(m) + R - 1) / R;  // rows per gather slot
   std::vector<size_t> rb(R), rc(R);
   for (int r = 0; r < R; r++) vs_dist_shard(m, R, r, &rb[r], &rc[r]);
   const size_t kn = static_cast<size_t>(k) * n;
-  RankBuffers dA, dB, dC, dG;
-  std::vector<size_t> abytes(R);
-  for (int r = 0; r < R; r++) abytes[r] = batch * rc[r] * k * sizeof(float);
+  // each rank holds only its rows of A and C and one copy of B
+  RankBuffers dA, dB, dC;
+  std::vector<size_t> abytes(R), cbytes(R);
+  for (int r = 0; r < R; r++) {
+    abytes[r] = batch * rc[r] * k * sizeof(float);
+    cbytes[r] = batch * rc[r] * n * sizeof(float);
+  }
   VS_TRY(dA.alloc(c, abytes));
   VS_TRY(dB.alloc(c, batch * kn * sizeof(float)));
-  VS_TRY(dC.alloc(c, batch * pad * n * sizeof(float)));
-  VS_TRY(dG.alloc(c, batch * R * pad * n * sizeof(float)));
-  // rows of A (contiguous per batch), B to rank 0 then broadcast
+  VS_TRY(dC.alloc(c, cbytes));
   for (int r = 0; r < R; r++)
     for (int b = 0; b < batch; b++)
       VS_TRY(h2d(c->dev[r], dA.f(r) + b * rc[r] * k,
                  A + (static_cast<size_t>(b) * m + rb[r]) * k, rc[r] * k * sizeof(float),
                  c->main[r]));
+  // B crosses PCIe once (to rank 0) and reaches the other ranks over xGMI
   VS_TRY(h2d(c->dev[0], dB.f(0), B, batch * kn * sizeof(float), c->main[0]));
   {
     auto p = dB.ptrs();
     VS_TRY(broadcast_on(c, c->main, p.data(), batch * kn * sizeof(float), 0));
   }
-  // per batch: GEMM on main, then all-gather of that batch on side
-  std::vector<std::vector<hipEvent_t>> evs(R, std::vector<hipEvent_t>(batch, nullptr));
+  // per matrix: the rank's rows on its main stream, then straight to the
+  // caller's C on the side stream (overlapping the next matrix's GEMM); the
+  // host receives every row block from the rank that computed it, so no
+  // device needs the whole C and nothing is gathered
+  std::vector<hipEvent_t> evs;
   struct EvFree {
-    std::vector<std::vector<hipEvent_t>> *e;
+    std::vector<hipEvent_t> *e;
     ~EvFree() {
-      for (auto &v : *e)
-        for (auto x : v)
-          if (x) (void)hipEventDestroy(x);
+      for (auto x : *e)
+        if (x) (void)hipEventDestroy(x);
     }
   } evfree{&evs};
+  for (int b = 0; b < batch; b++)
+    for (int r = 0; r < R; r++) {
+      if (rc[r] == 0) continue;
+      DevGuard g(c->dev[r]);
+      float *cb = dC.f(r) + b * rc[r] * n;
+      VS_TRY(vs_sgemm(0, 0, static_cast<int>(rc[r]), n, k, 1.f, dA.f(r) + b * rc[r] * k, k,
+                      dB.f(r) + b * kn, n, 0.f, cb, n, c->main[r]));
+      hipEvent_t ev = nullptr;
+      VS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      evs.push_back(ev);
+      VS_HIP(hipEventRecord(ev, c->main[r]));
+      VS_HIP(hipStreamWaitEvent(c->side[r], ev, 0));
+      VS_TRY(d2h(c->dev[r], C + (static_cast<size_t>(b) * m + rb[r]) * n, cb,
+                 rc[r] * n * sizeof(float), c->side[r]));
+    }
+  return vs_dist_synchronize(c);
+}
+
+vs_status vs_dist_sgemm_rowsplit_device(vs_dist_t c, int m, int n, int k,
+                                        const float *const *A, const float *const *B,
+                                        float *const *C, int batch) {
+  clear_error();
+  VS_TRY(check_ctx(c));
+  VS_REQUIRE(A && B && C, "vs_dist_sgemm_rowsplit_device: null pointer");
+  VS_REQUIRE(m > 0 && n > 0 && k > 0 && batch > 0, "vs_dist_sgemm_rowsplit_device: bad shape");
+  const int R = c->n;
+  std::vector<size_t> rb(R), rc(R);
+  for (int r = 0; r < R; r++) vs_dist_shard(m, R, r, &rb[r], &rc[r]);
+  for (int r = 0; r < R; r++)
+    VS_REQUIRE(A[r] && B[r] && C[r], "vs_dist_sgemm_rowsplit_device: rank %d null pointer", r);
+  const size_t kn = static_cast<size_t>(k) * n, mn = static_cast<size_t>(m) * n;
+  // matrix b: each rank writes its rows into its own full C, then the row
+  // blocks are all-gathered in place on the side stream while the next
+  // matrix's GEMM runs on the main stream
+  std::vector<hipEvent_t> evs;
+  struct EvFree {
+    std::vector<hipEvent_t> *e;
+    ~EvFree() {
+      for (auto x : *e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } evfree{&evs};
+  std::vector<size_t> off(R), bytes(R);
+  std::vector<void *> bufs(R);
   for (int b = 0; b < batch; b++) {
-    std::vector<const void *> send(R);
-    std::vector<void *> recv(R);
     for (int r = 0; r < R; r++) {
       DevGuard g(c->dev[r]);
-      float *cb = dC.f(r) + b * pad * n;
+      float *cb = C[r] + b * mn;
       if (rc[r] > 0)
-        VS_TRY(vs_sgemm(0, 0, static_cast<int>(rc[r]), n, k, 1.f, dA.f(r) + b * rc[r] * k, k,
-                        dB.f(r) + b * kn, n, 0.f, cb, n, c->main[r]));
-      VS_HIP(hipEventCreateWithFlags(&evs[r][b], hipEventDisableTiming));
-      VS_HIP(hipEventRecord(evs[r][b], c->main[r]));
-      VS_HIP(hipStreamWaitEvent(c->side[r], evs[r][b], 0));
-      send[r] = cb;
-      recv[r] = dG.f(r) + b * R * pad * n;
+        VS_TRY(vs_sgemm(0, 0, static_cast<int>(rc[r]), n, k, 1.f, A[r] + b * rc[r] * k, k,
+                        B[r] + b * kn, n, 0.f, cb + rb[r] * n, n, c->main[r]));
+      hipEvent_t ev = nullptr;
+      VS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      evs.push_back(ev);
+      VS_HIP(hipEventRecord(ev, c->main[r]));
+      VS_HIP(hipStreamWaitEvent(c->side[r], ev, 0));
+      bufs[r] = cb;
+      off[r] = rb[r] * n * sizeof(float);
+      bytes[r] = rc[r] * n * sizeof(float);
     }
-    VS_TRY(all_gather_on(c, c->side, send.data(), recv.data(), pad * n * sizeof(float)));
+    VS_TRY(all_gatherv_on(c, c->side, bufs.data(), off.data(), bytes.data()));
   }
-  // rank 0 holds every row block: [b][q][pad][n] -> C[b][rb[q]..][n]
-  for (int b = 0; b < batch; b++)
-    for (int q = 0; q < R; q++)
-      VS_TRY(d2h(c->dev[0], C + (static_cast<size_t>(b) * m + rb[q]) * n,
-                 dG.f(0) + (static_cast<size_t>(b) * R + q) * pad * n,
-                 rc[q] * n * sizeof(float), c->side[0]));
-  return vs_dist_synchronize(c);
+  // the caller's main streams see the gathered C
+  Events gathered(c);
+  VS_TRY(gathered.record(c->side));
+  for (int r = 0; r < R; r++) {
+    DevGuard g(c->dev[r]);
+    VS_TRY(gathered.wait(c->main[r], r));
+  }
+  return VS_OK;
 }
 
 vs_status vs_dist_conv1d_batch(vs_dist_t c, int correlate, const float *x, int x_len,

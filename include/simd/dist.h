@@ -6,7 +6,9 @@
  *  header is the native counterpart of its rows D2-D5:
  *    - D2 data parallel:     vs_dist_conv1d_batch (batch sharded over ranks);
  *    - D3 tensor parallel:   vs_dist_sgemm_rowsplit (A rows sharded, B
- *                            broadcast, C all-gathered, per-batch pipelined);
+ *                            broadcast, C rows downloaded per rank) and
+ *                            vs_dist_sgemm_rowsplit_device (C all-gathered
+ *                            in place on every GPU, per-matrix pipelined);
  *    - D4 context parallel:  vs_dist_conv1d_long / vs_dist_swt_long (long
  *                            signal split into contiguous chunks, halos
  *                            exchanged with neighbour send/recv);
@@ -81,14 +83,26 @@ vs_status vs_dist_halo_exchange(vs_dist_t ctx, const float *const *src,
                                 size_t halo_len, int direction, int periodic);
 
 /* ------------------------------ sharded entry points (host pointers in/out) */
-/// C[b] = A[b] @ B[b] for b < batch (row-major, A [batch][m][k], B
-/// [batch][k][n], C [batch][m][n]): rows of A split over ranks, B uploaded
-/// once to rank 0 and broadcast, C row blocks all-gathered batch by batch on
-/// a second stream per rank (overlapping batch b's gather with batch b+1's
-/// GEMM) and downloaded from rank 0.
+/// C[b] = A[b] @ B[b] for b < batch (row-major host arrays, A [batch][m][k],
+/// B [batch][k][n], C [batch][m][n]): rows of A split over ranks (each rank
+/// uploads and holds only its rows), B uploaded once to rank 0 and
+/// broadcast over xGMI, and each rank downloads its own C rows straight into
+/// the caller's C on a second stream, overlapping the next matrix's GEMM.
+/// No rank ever holds the whole C, so nothing is gathered.
 vs_status vs_dist_sgemm_rowsplit(vs_dist_t ctx, int m, int n, int k,
                                  const float *A, const float *B, float *C,
                                  int batch);
+/// Device-resident form for consumers that need the whole product on every
+/// GPU (BASELINE config 5): A[r] is rank r's rows ([batch][rows_r][k] on
+/// its device, rows_r from vs_dist_shard(m, size, r)), B[r] the full
+/// [batch][k][n] on rank r, C[r] a [batch][m][n] buffer on rank r.  Each
+/// rank computes its rows in place in its C[r]; the row blocks of matrix b
+/// are all-gathered in place (RCCL: one group of broadcasts, one root per
+/// rank) on the side streams while matrix b + 1 is multiplied.  Returns
+/// with every rank's main stream ordered after the gather.
+vs_status vs_dist_sgemm_rowsplit_device(vs_dist_t ctx, int m, int n, int k,
+                                        const float *const *A, const float *const *B,
+                                        float *const *C, int batch);
 /// Data-parallel batched convolution / correlation: rows of x [batch][x_len]
 /// sharded over ranks, one shared filter h, y [batch][x_len + h_len - 1].
 vs_status vs_dist_conv1d_batch(vs_dist_t ctx, int correlate, const float *x,

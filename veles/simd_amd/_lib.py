@@ -103,6 +103,7 @@ _SIGNATURES = {
     "vs_dist_all_reduce_sum": (_i, [_vp, _vp, _sz]),
     "vs_dist_halo_exchange": (_i, [_vp, _vp, _vp, _vp, _sz, _i, _i]),
     "vs_dist_sgemm_rowsplit": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i]),
+    "vs_dist_sgemm_rowsplit_device": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i]),
     "vs_dist_conv1d_batch": (_i, [_vp, _i, _vp, _i, _vp, _i, _vp, _i]),
     "vs_dist_conv1d_long": (_i, [_vp, _i, _vp, _sz, _vp, _i, _vp]),
     "vs_dist_swt_long": (_i, [_vp, _i, _i, _i, _i, _vp, _sz, _vp, _vp]),

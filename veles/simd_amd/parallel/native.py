@@ -127,6 +127,22 @@ class DeviceGroup:
                    "vs_dist_halo_exchange")
         self.synchronize()
 
+    def sgemm_rowsplit_device(self, a_rows, b, c) -> None:
+        """Device-resident row-split batched GEMM: a_rows[r] = rank r's rows
+        ([batch, rows_r, k], rows_r = shard(m, size, r)), b[r] = the full
+        [batch, k, n] and c[r] = a [batch, m, n] output on rank r's device;
+        on return every c[r] holds the whole product (rows all-gathered)."""
+        batch, _, k = a_rows[0].shape
+        m, n = c[0].shape[-2], c[0].shape[-1]
+        pa = _ptr_array([t.data_ptr() for t in a_rows])
+        pb = _ptr_array([t.data_ptr() for t in b])
+        pc = _ptr_array([t.data_ptr() for t in c])
+        self._sync_inputs(list(a_rows) + list(b))
+        _lib.check(_lib.lib().vs_dist_sgemm_rowsplit_device(self._h, m, n, k, pa, pb, pc,
+                                                            batch),
+                   "vs_dist_sgemm_rowsplit_device")
+        self.synchronize()
+
     @staticmethod
     def _sync_inputs(tensors) -> None:
         import torch

@@ -15,8 +15,22 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from .. import ops
+from .. import _lib, ops
+from ..ops._util import on_device, ptr, stream_of
 from . import comm
+
+
+def _sgemm_into(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> None:
+    """c = a @ b (2-D, contiguous, c possibly a row block of a larger
+    tensor) straight into c: no temporary, no copy."""
+    if not a.is_cuda:  # CPU / gloo test path: fp64-accumulated reference
+        c.copy_(ops.sgemm(a, b))
+        return
+    m, k = a.shape
+    n = b.shape[1]
+    with on_device(a):
+        _lib.call("vs_sgemm", 0, 0, m, n, k, 1.0, ptr(a), k, ptr(b), n, 0.0, ptr(c), n,
+                  stream_of(a))
 
 
 def rowsplit_bmm(a_local: torch.Tensor, b: torch.Tensor | None, *,
@@ -43,11 +57,15 @@ def rowsplit_bmm(a_local: torch.Tensor, b: torch.Tensor | None, *,
     if not gather or world == 1:
         if broadcast_src is not None and world > 1:
             dist.broadcast(b, broadcast_src)
-        return torch.stack([ops.sgemm(a_local[i], b[i]) for i in range(batch)]) \
-            if batch else a_local.new_empty((0, m_loc, n))
+        if out is None:
+            out = torch.empty((batch, m_loc, n), dtype=a_local.dtype, device=a_local.device)
+        for i in range(batch):
+            _sgemm_into(a_local[i].contiguous(), b[i].contiguous(), out[i])
+        return out
     if out is None:
         out = torch.empty((batch, m_loc * world, n), dtype=a_local.dtype,
                           device=a_local.device)
+    me = comm.rank()
     pending = []
     bcast = {}
 
@@ -60,7 +78,10 @@ def rowsplit_bmm(a_local: torch.Tensor, b: torch.Tensor | None, *,
         issue_bcast(i + 1)  # prefetch the next B while computing this one
         if i in bcast:
             bcast.pop(i).wait()
-        c_loc = ops.sgemm(a_local[i], b[i])
+        # this rank's rows written in place into its slot of out[i], then the
+        # in-place all-gather fills the other ranks' slots
+        c_loc = out[i, me * m_loc:(me + 1) * m_loc]
+        _sgemm_into(a_local[i].contiguous(), b[i].contiguous(), c_loc)
         pending.append((dist.all_gather_into_tensor(out[i], c_loc, async_op=True), c_loc))
         if len(pending) > 2:  # bound the number of in-flight result shards
             w, _ = pending.pop(0)
