@@ -28,7 +28,7 @@ extern "C" {
 #include <simd/wavelet.h>
 }
 #ifdef VELES_DEVICE
-#include <hip/hip_runtime_api.h>
+#include <hip/hip_runtime.h>
 #include <simd/gpu.h>
 #endif
 
@@ -135,6 +135,50 @@ void wavelet_rows(int scale) {
 }
 
 #ifdef VELES_DEVICE
+__global__ void empty_kernel() {}
+
+// Where a small host-API call's time goes: an empty launch + event wait
+// (the platform floor), a trivial host-API call (staging + dispatch), and
+// the device-resident single-signal convolutions (GPU execution latency of
+// the kernels themselves, one workgroup each).
+void floor_rows() {
+  hipStream_t s = nullptr;
+  hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  hipEvent_t ev;
+  hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  auto wait = [&] {
+    hipEventRecord(ev, s);
+    while (hipEventQuery(ev) == hipErrorNotReady) {
+    }
+  };
+  emit("floor_empty_launch_and_wait", time_us(20000, [&] {
+         hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s);
+         wait();
+       }));
+  std::vector<float> a(4, 1.f), b(4, 2.f), c(4);
+  emit("floor_host_api_matrix_add_2x2",
+       time_us(20000, [&] { matrix_add(1, a.data(), b.data(), 2, 2, c.data()); }));
+  for (int algo : {VS_CONV_DIRECT, VS_CONV_FFT}) {
+    float *x, *h, *y;
+    hipMalloc(&x, 4 * 512);
+    hipMalloc(&h, 4 * 512);
+    hipMalloc(&y, 4 * 1023);
+    hipMemset(x, 0, 4 * 512);
+    hipMemset(h, 0, 4 * 512);
+    emit(std::string("floor_device_conv_") + (algo == VS_CONV_FFT ? "fft" : "direct") +
+             "_512x512_single_call",
+         time_us(5000, [&] {
+           (void)vs_conv1d(algo, 0, x, 512, 512, h, 512, 0, y, 1023, 1, s);
+           wait();
+         }));
+    hipFree(x);
+    hipFree(h);
+    hipFree(y);
+  }
+  hipEventDestroy(ev);
+  hipStreamDestroy(s);
+}
+
 // Device-resident batched throughput: the same shapes, many signals per
 // launch, reported as microseconds per signal (per matrix product).
 void device_rows() {
@@ -217,6 +261,7 @@ int main(int argc, char **argv) {
   matrix_rows(scale);
   wavelet_rows(scale);
 #ifdef VELES_DEVICE
+  floor_rows();
   device_rows();
 #endif
   g_json += "}";

@@ -38,7 +38,7 @@ void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl
   const size_t yl = xl + hl - 1;
   vs::api::run_sync(what, [&](hipStream_t s) {
     Staged y(result, yl * 4, Staged::kOut, s);
-    Staged xx(x, xl * 4, Staged::kIn, s), hh(h, hl * 4, Staged::kIn, s);
+    Staged xx(x, xl * 4, Staged::kInReread, s), hh(h, hl * 4, Staged::kInReread, s);
     VS_TRY(y.status());
     VS_TRY(xx.status());
     VS_TRY(hh.status());

@@ -42,17 +42,14 @@ inline bool use_gpu_array(size_t n, std::initializer_list<const void *> ptrs) {
 
 // Runs body(stream) on the library stream and waits for it; aborts with the
 // library error message on failure (the host API has assert() semantics).
+// Host operands go through one packed CallStaging per call (one H2D, one
+// D2H, event polling; runtime.h).
 template <class F>
 void run_sync(const char *what, F &&body) {
   hipStream_t s = library_stream();
+  CallStaging staging(s);
   vs_status st = body(s);
-  if (st == VS_OK) {
-    hipError_t e = hipStreamSynchronize(s);
-    if (e != hipSuccess) {
-      set_error("hipStreamSynchronize: %s", hipGetErrorString(e));
-      st = VS_ERR_HIP;
-    }
-  }
+  if (st == VS_OK) st = staging.complete();
   if (st != VS_OK) fatal("%s: %s", what, last_error());
   log(2, "%s: done on GPU", what);
 }

@@ -55,8 +55,8 @@ void matrix_multiply(int simd, const float *m1, const float *m2, size_t w1,
   }
   vs::api::run_sync("matrix_multiply", [&](hipStream_t s) {
     Staged c(res, h1 * w2 * 4, Staged::kOut, s);
-    Staged a(m1, h1 * w1 * 4, Staged::kIn, s);
-    Staged b(m2, h2 * w2 * 4, Staged::kIn, s);
+    Staged a(m1, h1 * w1 * 4, Staged::kInReread, s);
+    Staged b(m2, h2 * w2 * 4, Staged::kInReread, s);
     VS_TRY(c.status());
     VS_TRY(a.status());
     VS_TRY(b.status());
@@ -79,8 +79,8 @@ void matrix_multiply_transposed(int simd, const float *m1, const float *m2,
   }
   vs::api::run_sync("matrix_multiply_transposed", [&](hipStream_t s) {
     Staged c(res, h1 * h2 * 4, Staged::kOut, s);
-    Staged a(m1, h1 * w1 * 4, Staged::kIn, s);
-    Staged b(m2, h2 * w2 * 4, Staged::kIn, s);
+    Staged a(m1, h1 * w1 * 4, Staged::kInReread, s);
+    Staged b(m2, h2 * w2 * 4, Staged::kInReread, s);
     VS_TRY(c.status());
     VS_TRY(a.status());
     VS_TRY(b.status());

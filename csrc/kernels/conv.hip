@@ -174,6 +174,61 @@ __global__ __launch_bounds__(kDirThreads) void direct_small_kernel(
   store_outputs(acc, sx, y + sig * ys, n0, q0, ylen);
 }
 
+// Small grids (few signals, short outputs, long filters -- e.g. one
+// 512 x 512 convolution, where direct_kernel is a single workgroup doing
+// 4096 serial FMAs per lane): 64 outputs per workgroup, the taps split over
+// its 8 waves.  The x window and taps are staged into LDS once (every load of
+// the fill in flight together), each wave accumulates its tap range with 4
+// independent chains, and the 8 partial sums are reduced through LDS.
+constexpr int kSplitWaves = 8;
+constexpr int kSplitMaxTaps = 4096;
+
+__global__ __launch_bounds__(64 * kSplitWaves) void direct_split_kernel(
+    const float *__restrict__ x, int xlen, int64_t xs, const float *__restrict__ h,
+    int hlen, int64_t hs, float *__restrict__ y, int64_t ys, int ylen, int reverse) {
+  __shared__ float sx[kSplitMaxTaps + 64];
+  __shared__ float sh[kSplitMaxTaps];
+  __shared__ float part[kSplitWaves][64];
+  const int sig = blockIdx.y;
+  const float *xrow = x + sig * xs;
+  const float *hrow = h + sig * hs;
+  const int n0 = blockIdx.x * 64;
+  // window: sx[i] = x[n0 - (hlen - 1) + i], i < hlen + 63
+  const int xbase = n0 - (hlen - 1);
+#pragma unroll 4
+  for (int i = threadIdx.x; i < hlen + 63; i += 64 * kSplitWaves) {
+    const int p = xbase + i;
+    sx[i] = (p >= 0 && p < xlen) ? xrow[p] : 0.f;
+  }
+#pragma unroll 4
+  for (int i = threadIdx.x; i < hlen; i += 64 * kSplitWaves)
+    sh[i] = reverse ? hrow[hlen - 1 - i] : hrow[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = (hlen + kSplitWaves - 1) / kSplitWaves;
+  const int m0 = wave * per, m1 = min(hlen, m0 + per);
+  // y[n0 + lane] = sum_m sh[m] * sx[lane + hlen - 1 - m]
+  const float *wl = sx + lane + hlen - 1;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int m = m0;
+  for (; m + 4 <= m1; m += 4) {
+    a0 = fmaf(sh[m], wl[-m], a0);
+    a1 = fmaf(sh[m + 1], wl[-m - 1], a1);
+    a2 = fmaf(sh[m + 2], wl[-m - 2], a2);
+    a3 = fmaf(sh[m + 3], wl[-m - 3], a3);
+  }
+  for (; m < m1; m++) a0 = fmaf(sh[m], wl[-m], a0);
+  part[wave][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wave == 0 && n0 + lane < ylen) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kSplitWaves; w++) t += part[w][lane];
+    y[sig * ys + n0 + lane] = t;
+  }
+}
+
 // ------------------------------------------------------ filter spectrum
 // hc[f][n] = (reversed?) h[f][n] + 0i for n < hlen, 0 beyond (length L).
 __global__ __launch_bounds__(256) void pad_filter_kernel(
@@ -806,6 +861,11 @@ vs_status run_direct(int correlate, const float *x, int xlen, int64_t xs,
   else if (hlen <= 32)
     hipLaunchKernelGGL(direct_small_kernel<32>, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
                        hlen, hs, y, ys, ylen, correlate);
+  else if (hlen <= kSplitMaxTaps &&
+           static_cast<int64_t>(grid.x) * batch < 2 * device_cu_count())
+    hipLaunchKernelGGL(direct_split_kernel, dim3((ylen + 63) / 64, batch),
+                       dim3(64 * kSplitWaves), 0, s, x, xlen, xs, h, hlen, hs, y, ys, ylen,
+                       correlate);
   else
     hipLaunchKernelGGL(direct_kernel, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
                        hlen, hs, y, ys, ylen, correlate);

@@ -4,6 +4,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -308,6 +309,132 @@ void DeviceBuffer::release() {
 
 void release_cached_memory() { ScratchPool::get().release_all_free(); }
 
+// ------------------------------------------------------- packed staging
+namespace {
+
+// Per thread: a pinned, device-mapped host arena and a device arena of the
+// same size.  Small operands of a call live in them for the duration of the
+// call:
+//   * zero-copy operands (read or written once per element, e.g. the
+//     elementwise maps and every output): kernels access the pinned image
+//     directly over the host link -- no DMA set-up at all;
+//   * re-read inputs (convolution windows, GEMM panels, read by many
+//     workgroups): packed into the pinned image and sent to the device
+//     image with ONE host->device copy before the first kernel reads them.
+// Round 1 staged every operand through its own pageable copy (HIP bounces
+// each through an internal buffer) and ended with a blocking stream
+// synchronise: ~40-65 us per call.
+struct Arena {
+  char *host = nullptr, *mapped = nullptr, *dev = nullptr;  // mapped = host, device view
+  size_t cap = 0;
+  int device = -1;
+};
+
+constexpr size_t kStageMax = 64 << 10;    // per operand
+constexpr size_t kArenaBytes = 4 << 20;   // per thread
+
+thread_local Arena t_arena;
+thread_local CallStaging *t_call = nullptr;
+
+bool arena_ready() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Arena &a = t_arena;
+  if (a.host && a.device == dev) return true;
+  if (a.host) (void)hipHostFree(a.host);
+  if (a.dev) (void)hipFree(a.dev);
+  a = Arena{};
+  void *h = nullptr, *m = nullptr, *d = nullptr;
+  if (hipHostMalloc(&h, kArenaBytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(&m, h, 0) != hipSuccess || hipMalloc(&d, kArenaBytes) != hipSuccess) {
+    (void)hipGetLastError();
+    if (h) (void)hipHostFree(h);
+    return false;
+  }
+  a.host = static_cast<char *>(h);
+  a.mapped = static_cast<char *>(m);
+  a.dev = static_cast<char *>(d);
+  a.cap = kArenaBytes;
+  a.device = dev;
+  return true;
+}
+
+bool zero_copy_enabled() {
+  static const bool v = env_int("VELES_ZERO_COPY", 1) != 0;
+  return v;
+}
+
+}  // namespace
+
+CallStaging::CallStaging(hipStream_t s) : stream_(s), prev_(t_call) { t_call = this; }
+CallStaging::~CallStaging() { t_call = prev_; }
+CallStaging *CallStaging::current() { return t_call; }
+
+void *CallStaging::reserve(const void *host_in, size_t bytes, bool zero_copy) {
+  if (bytes == 0 || bytes > kStageMax) return nullptr;
+  const size_t off = (used_ + 255) & ~size_t{255};
+  if (!arena_ready() || off + bytes > t_arena.cap) return nullptr;
+  used_ = off + bytes;
+  if (host_in) std::memcpy(t_arena.host + off, host_in, bytes);
+  if (zero_copy && zero_copy_enabled()) return t_arena.mapped + off;
+  if (host_in) {
+    if (pend_hi_ == pend_lo_) pend_lo_ = off;
+    pend_hi_ = off + bytes;
+  }
+  return t_arena.dev + off;
+}
+
+vs_status CallStaging::flush() {
+  if (pend_hi_ == pend_lo_) return VS_OK;
+  const size_t lo = pend_lo_, n = pend_hi_ - pend_lo_;
+  pend_lo_ = pend_hi_ = 0;
+  VS_HIP(hipMemcpyAsync(t_arena.dev + lo, t_arena.host + lo, n, hipMemcpyHostToDevice,
+                        stream_));
+  return VS_OK;
+}
+
+void CallStaging::add_output(void *dev, void *host, size_t bytes) {
+  char *p = static_cast<char *>(dev);
+  const bool mapped = p >= t_arena.mapped && p < t_arena.mapped + t_arena.cap;
+  outs_.push_back(Out{static_cast<size_t>(p - (mapped ? t_arena.mapped : t_arena.dev)), bytes,
+                      host, mapped});
+}
+
+vs_status CallStaging::complete() {
+  VS_TRY(flush());
+  // device-image outputs (none unless zero-copy is off) come back first
+  for (const Out &o : outs_)
+    if (!o.mapped)
+      VS_HIP(hipMemcpyAsync(t_arena.host + o.off, t_arena.dev + o.off, o.bytes,
+                            hipMemcpyDeviceToHost, stream_));
+  VS_TRY(wait_stream(stream_));
+  for (const Out &o : outs_) std::memcpy(o.host, t_arena.host + o.off, o.bytes);
+  outs_.clear();
+  return VS_OK;
+}
+
+vs_status wait_stream(hipStream_t s) {
+  thread_local hipEvent_t ev = nullptr;
+  thread_local int ev_dev = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (ev && ev_dev != dev) {
+    (void)hipEventDestroy(ev);
+    ev = nullptr;
+  }
+  if (!ev) {
+    VS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ev_dev = dev;
+  }
+  VS_HIP(hipEventRecord(ev, s));
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return VS_OK;
+    if (e != hipErrorNotReady) return hip_status(e, "hipEventQuery", __FILE__, __LINE__);
+  }
+}
+
 Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)
     : user_(const_cast<void *>(user)), bytes_(bytes), dir_(dir),
       stream_(stream) {
@@ -317,6 +444,16 @@ Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)
     return;
   }
   log(2, "stage %p (%zu B): host buffer, dir=%d", user, bytes, static_cast<int>(dir));
+  if (CallStaging *cs = CallStaging::current(); cs && !sync_stage()) {
+    // inputs re-read by many workgroups go to device memory; outputs and
+    // read-once inputs stay in the mapped host image
+    const bool zero_copy = !(dir & kIn) || !(dir & kReread);
+    if (void *d = cs->reserve((dir & kIn) ? user : nullptr, bytes, zero_copy)) {
+      dev_ = d;
+      packed_ = true;
+      return;
+    }
+  }
   status_ = buf_.alloc(bytes, stream);
   if (status_ != VS_OK) return;
   dev_ = buf_.get();
@@ -333,6 +470,10 @@ Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)
 vs_status Staged::finish() {
   if (status_ != VS_OK) return status_;
   if (dev_ == user_ || !(dir_ & kOut) || !bytes_) return VS_OK;
+  if (packed_) {
+    CallStaging::current()->add_output(dev_, user_, bytes_);
+    return VS_OK;
+  }
   if (sync_stage())
     VS_HIP(hipMemcpyWithStream(user_, dev_, bytes_, hipMemcpyDeviceToHost, stream_));
   else

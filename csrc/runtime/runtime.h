@@ -13,6 +13,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "simd/gpu.h"
 
@@ -128,16 +129,60 @@ class DeviceBuffer {
 void release_cached_memory();
 
 // ----------------------------------------------------------- staging
+// Staging context of one host-API call (api::run_sync opens one per call).
+// Host operands of up to 64 KiB live in a pinned, device-mapped arena of the
+// calling thread for the call: outputs and read-once inputs are accessed
+// there by the kernels directly (zero-copy); inputs re-read by many
+// workgroups (Staged::kReread) are packed and sent to a device arena with
+// ONE host->device copy before the first kernel reads them.  The call ends
+// with one event wait and the copies to the caller's buffers.  Larger
+// operands take the per-operand copy path; VELES_ZERO_COPY=0 moves every
+// small operand to the device arena.
+class CallStaging {
+ public:
+  explicit CallStaging(hipStream_t s);
+  ~CallStaging();
+  CallStaging(const CallStaging &) = delete;
+  CallStaging &operator=(const CallStaging &) = delete;
+  static CallStaging *current();
+  // Reserves `bytes` in the arena (input: copied into the pinned image now);
+  // returns the address kernels use (mapped host image when zero_copy, else
+  // the device image), or nullptr (operand too large / arena full).
+  void *reserve(const void *host_in, size_t bytes, bool zero_copy);
+  // Issues the pending host->device copy of the re-read inputs.
+  vs_status flush();
+  // Output region [dev, dev + bytes) goes to `host` after the call.
+  void add_output(void *dev, void *host, size_t bytes);
+  // Event wait, then the outputs to the caller's buffers.
+  vs_status complete();
+
+ private:
+  struct Out {
+    size_t off, bytes;
+    void *host;
+    bool mapped;
+  };
+  hipStream_t stream_;
+  CallStaging *prev_;
+  size_t used_ = 0, pend_lo_ = 0, pend_hi_ = 0;
+  std::vector<Out> outs_;
+};
+
 // Presents a host-or-device operand as a device pointer on `stream`.
 // Device pointers pass through; host buffers are copied in (kIn), out on
-// finish() (kOut) or both.
+// finish() (kOut) or both -- through the call's CallStaging when one is open.
 class Staged {
  public:
-  enum Dir { kIn = 1, kOut = 2, kInOut = 3 };
+  // kReread: an input that many workgroups read (convolution windows, GEMM
+  // panels) -- staged into device memory, never read over the host link.
+  enum Dir { kIn = 1, kOut = 2, kInOut = 3, kReread = 4, kInReread = 5 };
   Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream);
   vs_status status() const { return status_; }
   template <class T>
   T *dev() const {
+    // the packed copy of the call's inputs goes out before any kernel can
+    // read this pointer
+    if (packed_) (void)CallStaging::current()->flush();
     return static_cast<T *>(dev_);
   }
   // Copies device results back to the host buffer (kOut / kInOut).
@@ -151,6 +196,11 @@ class Staged {
   hipStream_t stream_;
   DeviceBuffer buf_;
   vs_status status_ = VS_OK;
+  bool packed_ = false;  // lives in the call's CallStaging arena
 };
+
+// Waits for everything queued on `s` so far by polling an event (lower
+// latency than a blocking stream synchronise on a short call).
+vs_status wait_stream(hipStream_t s);
 
 }  // namespace vs

@@ -141,3 +141,12 @@ def test_select_never_unsupported():
     for xlen, hlen in [(1 << 26, 3), (1 << 26, 5000), (1 << 26, 40000), (1 << 24, 1 << 20),
                        (1 << 20, 1 << 20), (10, 10 ** 6)]:
         assert _lib.lib().vs_conv1d_select(xlen, hlen, 1) in (1, 2, 3)
+
+
+@pytest.mark.parametrize("xlen,hlen,batch", [(512, 512, 1), (1000, 33, 2), (300, 1000, 1),
+                                             (5000, 4096, 1), (20000, 777, 3), (17, 40, 2)])
+@pytest.mark.parametrize("corr", [False, True])
+def test_direct_small_grid(xlen, hlen, batch, corr):
+    """Tap-split direct kernel (conv.hip direct_split_kernel): grids smaller
+    than two workgroups per CU with 32 < h <= 4096."""
+    _check(xlen, hlen, batch, "direct", corr, rel=1e-6)

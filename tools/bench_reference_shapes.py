@@ -58,6 +58,7 @@ def build():
                        + ["-o", os.path.join(OUT, "ref_shapes_reference"), "-lm"], check=True)
     lib = os.path.join(REPO, "veles", "simd_amd", "_native")
     subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-DVELES_DEVICE",
+                    "--offload-arch=gfx950", "-x", "hip",
                     "-I" + os.path.join(REPO, "include"),
                     os.path.join(REPO, "bench", "ref_shapes.cc"), "-L" + lib, "-lvelessimd",
                     "-Wl,-rpath," + lib, "-o", os.path.join(OUT, "ref_shapes_veles")], check=True)
