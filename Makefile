@@ -57,6 +57,46 @@ $(TEST_BIN): tests/native/capi_test.cpp $(LIB) $(HEADERS)
 clean:
 	rm -rf $(BUILD) $(LIB)
 
+# Install: library + the 18 public headers + pkg-config file, the layout of
+# the reference's `make install` (/root/reference/inc/Makefile.am:27-31,
+# src/Makefile.am:29, Simd.pc.in).  The library is also installed as
+# libSimd.so and the .pc as Simd.pc, so `pkg-config --cflags --libs Simd`
+# and `-lSimd` consumers of the reference link unchanged.
+#   make install PREFIX=/opt/veles [DESTDIR=/tmp/stage]
+PREFIX     ?= /usr/local
+DESTDIR    ?=
+VERSION    := $(shell sed -n 's/^__version__ = "\(.*\)"/\1/p' veles/simd_amd/__init__.py)
+INST_LIB   := $(DESTDIR)$(PREFIX)/lib
+INST_INC   := $(DESTDIR)$(PREFIX)/include/simd
+INST_PC    := $(INST_LIB)/pkgconfig
+install: $(LIB)
+	install -d $(INST_LIB) $(INST_INC) $(INST_PC)
+	install -m 0755 $(LIB) $(INST_LIB)/libvelessimd.so.$(VERSION)
+	ln -sf libvelessimd.so.$(VERSION) $(INST_LIB)/libvelessimd.so
+	ln -sf libvelessimd.so.$(VERSION) $(INST_LIB)/libSimd.so
+	install -m 0644 include/simd/*.h $(INST_INC)/
+	sed -e 's|@prefix@|$(PREFIX)|' -e 's|@libdir@|$(PREFIX)/lib|' \
+	    -e 's|@includedir@|$(PREFIX)/include|' -e 's|@VERSION@|$(VERSION)|' \
+	    -e 's|@rocmlib@|/opt/rocm/lib|' simd.pc.in > $(INST_PC)/Simd.pc
+	ln -sf Simd.pc $(INST_PC)/veles-simd-amd.pc
+
+uninstall:
+	rm -f $(INST_LIB)/libvelessimd.so* $(INST_LIB)/libSimd.so $(INST_PC)/Simd.pc \
+	    $(INST_PC)/veles-simd-amd.pc
+	rm -rf $(INST_INC)
+
+# Static analysis (clang analyzer + strict warnings, host side of every
+# source); report in build/lint/report.txt.
+lint:
+	bash tools/lint.sh
+
+# API reference (Doxygen, if installed) into build/docs.
+docs:
+	@command -v doxygen >/dev/null || { echo "doxygen not installed"; exit 1; }
+	mkdir -p $(BUILD)/docs && doxygen docs/Doxyfile
+
+.PHONY: install uninstall lint docs
+
 # Host AddressSanitizer build of the library + native C API test (host code
 # only: device ASan / XNACK is not available on the GPU pool).  Runs the
 # host-reference paths on any machine: `make asan && ASAN_OPTIONS=detect_leaks=1 \

@@ -33,17 +33,20 @@ int next_pow2_ge(size_t n) {
   return p;
 }
 
+using vs::api::checked_int;
+
 void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl,
               const float *h, size_t hl, float *result) {
   const size_t yl = xl + hl - 1;
+  (void)checked_int(what, yl);
   vs::api::run_sync(what, [&](hipStream_t s) {
     Staged y(result, yl * 4, Staged::kOut, s);
     Staged xx(x, xl * 4, Staged::kInReread, s), hh(h, hl * 4, Staged::kInReread, s);
     VS_TRY(y.status());
     VS_TRY(xx.status());
     VS_TRY(hh.status());
-    VS_TRY(vs_conv1d(algo, reverse, xx.dev<float>(), static_cast<int>(xl),
-                     static_cast<int64_t>(xl), hh.dev<float>(), static_cast<int>(hl),
+    VS_TRY(vs_conv1d(algo, reverse, xx.dev<float>(), checked_int(what, xl),
+                     static_cast<int64_t>(xl), hh.dev<float>(), checked_int(what, hl),
                      0, y.dev<float>(), static_cast<int64_t>(yl), 1, s));
     return y.finish();
   });
@@ -67,7 +70,7 @@ ConvPlan *make_plan(int algo, size_t xl, size_t hl) {
   p->x_length = xl;
   p->h_length = hl;
   p->block = algo == VS_CONV_OVERLAP_SAVE
-                 ? vs_conv1d_os_block(static_cast<int>(hl))
+                 ? vs_conv1d_os_block(checked_int("convolution", hl))
                  : next_pow2_ge(xl + hl - 1);
   return p;
 }
@@ -80,8 +83,8 @@ ConvolutionFFTHandle fft_init(size_t xl, size_t hl, int reverse) {
   h.fft_inverse_plan = p;
   h.M = static_cast<int *>(std::malloc(sizeof(int)));
   *h.M = p->block;
-  h.x_length = static_cast<int>(xl);
-  h.h_length = static_cast<int>(hl);
+  h.x_length = checked_int("convolve_fft_initialize", xl);
+  h.h_length = checked_int("convolve_fft_initialize", hl);
   h.inputs = nullptr;
   h.reverse = reverse;
   return h;
@@ -117,11 +120,11 @@ void os_fini(ConvolutionOverlapSaveHandle h) {
 ConvolutionHandle auto_init(size_t xl, size_t hl, int reverse) {
   ConvolutionHandle h;
   std::memset(&h, 0, sizeof(h));
-  h.x_length = static_cast<int>(xl);
-  h.h_length = static_cast<int>(hl);
+  h.x_length = checked_int("convolve_initialize", xl);
+  h.h_length = checked_int("convolve_initialize", hl);
   int algo;
   if (vs::gpu_available()) {
-    algo = vs_conv1d_select(static_cast<int>(xl), static_cast<int>(hl), 1);
+    algo = vs_conv1d_select(h.x_length, h.h_length, 1);
     if (algo == VS_CONV_OVERLAP_SAVE && !(hl < xl / 2)) algo = VS_CONV_FFT;
   } else {
     // reference heuristic (src/convolve.c:349-363)

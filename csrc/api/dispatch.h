@@ -11,6 +11,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <climits>
+#include <cstddef>
 #include <initializer_list>
 
 #include "csrc/runtime/runtime.h"
@@ -22,6 +24,14 @@ inline bool any_device(std::initializer_list<const void *> ptrs) {
   for (const void *p : ptrs)
     if (is_device_pointer(p)) return true;
   return false;
+}
+
+// The device API takes int dimensions: refuse, loudly, any size it cannot
+// represent instead of truncating it (the reference API is size_t).
+inline int checked_int(const char *what, size_t n) {
+  if (n > static_cast<size_t>(INT_MAX))
+    fatal("%s: size %zu exceeds the device path limit of %d", what, n, INT_MAX);
+  return static_cast<int>(n);
 }
 
 inline bool use_gpu_simd(int simd, const char *fn) {

@@ -60,8 +60,8 @@ void matrix_multiply(int simd, const float *m1, const float *m2, size_t w1,
     VS_TRY(c.status());
     VS_TRY(a.status());
     VS_TRY(b.status());
-    VS_TRY(vs_sgemm(0, 0, static_cast<int>(h1), static_cast<int>(w2),
-                    static_cast<int>(w1), 1.f, a.dev<float>(), w1,
+    VS_TRY(vs_sgemm(0, 0, vs::api::checked_int("matrix_multiply", h1), vs::api::checked_int("matrix_multiply", w2),
+                    vs::api::checked_int("matrix_multiply", w1), 1.f, a.dev<float>(), w1,
                     b.dev<float>(), w2, 0.f, c.dev<float>(), w2, s));
     return c.finish();
   });
@@ -84,8 +84,8 @@ void matrix_multiply_transposed(int simd, const float *m1, const float *m2,
     VS_TRY(c.status());
     VS_TRY(a.status());
     VS_TRY(b.status());
-    VS_TRY(vs_sgemm(0, 1, static_cast<int>(h1), static_cast<int>(h2),
-                    static_cast<int>(w1), 1.f, a.dev<float>(), w1,
+    VS_TRY(vs_sgemm(0, 1, vs::api::checked_int("matrix_multiply", h1), vs::api::checked_int("matrix_multiply", h2),
+                    vs::api::checked_int("matrix_multiply", w1), 1.f, a.dev<float>(), w1,
                     b.dev<float>(), w2, 0.f, c.dev<float>(), h2, s));
     return c.finish();
   });

@@ -90,7 +90,7 @@ void minmax1D(int simd, const float *src, int n, float *mn, float *mx) {
     vs::ref::minmax1d(src, n, mn, mx);
     return;
   }
-  float out[2];
+  float out[2] = {0.f, 0.f};
   vs::api::run_sync("minmax1D", [&](hipStream_t s) {
     Staged x(src, static_cast<size_t>(n) * 4, Staged::kIn, s);
     Staged o(out, 8, Staged::kOut, s);

@@ -236,7 +236,7 @@ __device__ __forceinline__ void dma_image(const uint16_t *__restrict__ img, int6
     const int pc = lane % C::NC;                // physical chunk it fills
     const int c = swz<C>(row, pc);              // logical chunk stored there
     const uint16_t *src = img + static_cast<int64_t>(row0 + row) * ld + k0 + 8 * c;
-    __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)(dst + j * 1024), 16, 0,
+    __builtin_amdgcn_global_load_lds((glob_void *)const_cast<uint16_t *>(src), (lds_void *)(dst + j * 1024), 16, 0,
                                      0);
   }
 }

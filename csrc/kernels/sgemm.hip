@@ -217,13 +217,13 @@ __global__ __launch_bounds__(C::kThreads) void sgemm5_kernel(GemmArgs g) {
     uint8_t *base = smem5 + st * C::kStage;
 #pragma unroll
     for (int i = 0; i < C::kInstrA; i++)
-      __builtin_amdgcn_global_load_lds((glob_void_t *)(pa[i] + kt * C::BK),
+      __builtin_amdgcn_global_load_lds((glob_void_t *)const_cast<float *>(pa[i] + kt * C::BK),
                                        (lds_void_t *)(base + (wid * C::kInstrA + i) * 1024),
                                        16, 0, 0);
 #pragma unroll
     for (int i = 0; i < C::kInstrB; i++)
       __builtin_amdgcn_global_load_lds(
-          (glob_void_t *)(pb[i] + static_cast<int64_t>(kt) * C::BK * g.ldb),
+          (glob_void_t *)const_cast<float *>(pb[i] + static_cast<int64_t>(kt) * C::BK * g.ldb),
           (lds_void_t *)(base + C::kImgA + (wid * C::kInstrB + i) * 1024), 16, 0, 0);
   };
 

@@ -165,9 +165,20 @@ def check(status: int, what: str = "") -> None:
         raise VelesError(f"{what or 'native call'} failed (status {status}): {msg}")
 
 
+_RANGES = os.environ.get("VELES_PROFILE_RANGES", "0") == "1"
+
+
 def call(name: str, *args) -> None:
-    """Call a vs_* function and raise VelesError on a non-zero status."""
+    """Call a vs_* function and raise VelesError on a non-zero status.
+    With VELES_PROFILE_RANGES=1 each call is a roctx range named after the
+    function (utils/profiling.py), so rocprofv3 --marker-trace timelines show
+    which op launched which kernels."""
     fn = getattr(lib(), name)
+    if _RANGES:
+        from .utils.profiling import trace_range
+        with trace_range(name):
+            check(fn(*args), name)
+        return
     check(fn(*args), name)
 
 

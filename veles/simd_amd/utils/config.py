@@ -1,32 +1,67 @@
-"""Runtime configuration knobs (environment variables read by the native
-library and the Python layer).  The reference is configured only at build
-time (autotools flags); these are the runtime equivalents."""
+"""Runtime configuration knobs: the environment variables read by the native
+library (csrc/) and the Python layer, with their defaults and meaning.
+
+The reference is configured only at build time (autotools flags, SURVEY.md
+§5); these are the runtime equivalents.  ``KNOBS`` is the single registry:
+tests/test_config.py checks that every variable the native sources read is
+listed here, and ``python -m veles.simd_amd.utils.config`` prints the
+effective values of the current environment."""
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 
 @dataclass(frozen=True)
-class Config:
-    log_level: int = field(default_factory=lambda: int(os.environ.get("VELES_LOG_LEVEL", "0")))
-    gpu_min_elems: int = field(
-        default_factory=lambda: int(os.environ.get("VELES_GPU_MIN_ELEMS", str(1 << 20))))
-    disable_gpu: bool = field(
-        default_factory=lambda: os.environ.get("VELES_DISABLE_GPU", "0") == "1")
-    sgemm_variant: int = field(
-        default_factory=lambda: int(os.environ.get("VELES_SGEMM_VARIANT", "-1")))
-    profile_ranges: bool = field(
-        default_factory=lambda: os.environ.get("VELES_PROFILE_RANGES", "0") == "1")
+class Knob:
+    name: str
+    default: str
+    doc: str
+    where: str  # the file that reads it
 
-    DOC = {
-        "VELES_LOG_LEVEL": "0 quiet, 1 dispatch decisions, 2 verbose (native stderr)",
-        "VELES_GPU_MIN_ELEMS": "host arrays at least this long run on the GPU "
-                               "(flag-less arithmetic.h functions)",
-        "VELES_DISABLE_GPU": "1: behave as if no GPU were present",
-        "VELES_SGEMM_VARIANT": "force an SGEMM tile variant (0..4) for tuning",
-        "VELES_PROFILE_RANGES": "1: emit roctx ranges around Python-level ops",
-    }
+    @property
+    def value(self) -> str:
+        return os.environ.get(self.name, self.default)
 
 
-config = Config()
+KNOBS = [
+    Knob("VELES_LOG_LEVEL", "0", "0 quiet, 1 dispatch decisions, 2 every staging step "
+         "(native stderr)", "csrc/runtime/runtime.cpp"),
+    Knob("VELES_DISABLE_GPU", "0", "1: behave as if no GPU were present (host reference "
+         "paths)", "csrc/runtime/runtime.cpp"),
+    Knob("VELES_GPU_MIN_ELEMS", str(1 << 20), "host arrays of at least this many elements "
+         "(x taps for wavelets) run on the GPU in the flag-less API", "csrc/runtime/runtime.cpp"),
+    Knob("VELES_HOST_MAX_MACS", str(1 << 17), "direct convolutions of host operands below "
+         "this many multiply-adds run on the host even with simd=1", "csrc/api/convolve.cpp"),
+    Knob("VELES_SYNC_STAGE", "0", "1: stage host operands with synchronous copies (debug)",
+         "csrc/runtime/runtime.cpp"),
+    Knob("VELES_ZERO_COPY", "1", "0: stage every small host operand into device memory "
+         "instead of the mapped pinned arena", "csrc/runtime/runtime.cpp"),
+    Knob("VELES_SGEMM_VARIANT", "-1", "force an SGEMM kernel variant "
+         "(0..VS_SGEMM_VARIANTS-1, include/simd/gpu.h) for tuning", "csrc/kernels/sgemm.hip"),
+    Knob("VELES_GEMM_BF16_VARIANT", "-1", "force a bf16 GEMM variant (0: 128 tiles, "
+         "1: large tiles)", "csrc/kernels/gemm_bf16.hip"),
+    Knob("VELES_GEMM_BF16_PACK", "-1", "force (1) or forbid (0) the bf16 operand pre-pack "
+         "pass", "csrc/kernels/gemm_bf16.hip"),
+    Knob("VELES_DIST_TIMEOUT_MS", "300000", "RCCL watchdog timeout of vs_dist_synchronize",
+         "csrc/dist/dist.cpp"),
+    Knob("VS_EW_GRID_CAP", str(1 << 20), "elementwise grid cap in workgroups (grid-stride "
+         "beyond; tuning)", "csrc/runtime/runtime.cpp"),
+    Knob("VELES_PROFILE_RANGES", "0", "1: roctx range around every native call made from "
+         "Python (visible in rocprofv3 --marker-trace)", "veles/simd_amd/_lib.py"),
+    Knob("VELES_SIMD_LIB", "", "path of an alternative libvelessimd.so (A/B runs)",
+         "veles/simd_amd/_lib.py"),
+]
+BY_NAME = {k.name: k for k in KNOBS}
+
+
+def describe() -> str:
+    """Markdown table of every knob with its effective value."""
+    rows = ["| variable | value | default | meaning |", "|---|---|---|---|"]
+    for k in KNOBS:
+        rows.append(f"| `{k.name}` | {k.value or '-'} | {k.default or '-'} | {k.doc} |")
+    return "\n".join(rows)
+
+
+if __name__ == "__main__":
+    print(describe())
