@@ -150,3 +150,11 @@ def test_direct_small_grid(xlen, hlen, batch, corr):
     """Tap-split direct kernel (conv.hip direct_split_kernel): grids smaller
     than two workgroups per CU with 32 < h <= 4096."""
     _check(xlen, hlen, batch, "direct", corr, rel=1e-6)
+
+
+@pytest.mark.parametrize("hlen", [33, 600, 5000])
+def test_direct_large_grid(hlen):
+    """Register-blocked direct kernel (conv.hip direct_kernel): grids of at
+    least two workgroups per CU, filters over one 512-tap LDS chunk too."""
+    _check(300000, hlen, 4, "direct", False, rel=1e-6)
+    _check(300000, hlen, 4, "direct", True, rel=1e-6)
