@@ -1062,6 +1062,13 @@ vs_status run_fft_large(int correlate, const float *x, int xlen, int64_t xs,
 }  // namespace conv
 }  // namespace vs
 
+// vs_tune_set keys of the wavelet kernels (wavelet.hip)
+namespace vs {
+namespace wav {
+bool tune(const char *key, int value);
+}
+}  // namespace vs
+
 using namespace vs;
 
 extern "C" {
@@ -1178,6 +1185,7 @@ vs_status vs_tune_set(const char *key, int value) {
     conv::g_conv_real_all = value != 0;
     return VS_OK;
   }
+  if (wav::tune(key, value)) return VS_OK;
   set_error("vs_tune_set: unknown key '%s'", key);
   return VS_ERR_INVALID;
 }

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 
 #include "csrc/data/wavelet_tables.h"
 #include "csrc/kernels/device.h"
@@ -282,6 +283,167 @@ __global__ __launch_bounds__(256) void swt_multi4_kernel(
     lrow[q] = reinterpret_cast<const float4 *>(in)[q];
 }
 
+// Round-2 multi-level kernel.  Same mapping as
+// swt_multi4_kernel, but the boundary extension of the next level's input is
+// written by the lanes that produce it, in the same pass:
+//   periodic: in[len + t] = in[t]          -> the float4 at i0 < halo is also
+//                                              stored at len + i0;
+//   mirror:   in[len + t] = in[len - 1 - t] -> the float4 at i0 is stored
+//                                              reversed at 2 len - 4 - i0;
+//   zero:     the halo regions are zeroed once;
+//   constant: one broadcast fill phase per level (the only extra barrier).
+// No modulo / per-element extension code runs, each level costs one barrier,
+// and the last level writes the low band straight to HBM.  Needs
+// len % 4 == 0.
+// PMC (db16, 16384 x 1024): the old kernel issued ~4x the VALU instructions
+// of its FMAs, most of them in the modulo halo fill
+// (profiles/r2/swt/README.md).
+template <int ORDER, bool NT>
+__global__ __launch_bounds__(256) void swt_fused_kernel(
+    Taps taps, int ext, int levels, const float *__restrict__ src, int len,
+    float *__restrict__ hi, float *__restrict__ lo) {
+  extern __shared__ __attribute__((aligned(16))) float smemf[];
+  const int stride = (len + ((ORDER - 1) << (levels - 1)) + 2 * ORDER + 8 + 3) & ~3;
+  float *band0 = smemf, *band1 = smemf + stride;
+  const int64_t sig = blockIdx.x;
+  const int len4 = len >> 2;
+  float hp[ORDER], lp[ORDER];
+#pragma unroll
+  for (int r = 0; r < ORDER; r++) {
+    hp[r] = taps.hp[r];
+    lp[r] = taps.lp[r];
+  }
+  if (ext == EXTENSION_TYPE_ZERO) {
+    const int z4 = (stride - len) >> 2;
+    for (int i = threadIdx.x; i < 2 * z4; i += blockDim.x)
+      reinterpret_cast<float4 *>(i < z4 ? band0 + len : band1 + len)[i < z4 ? i : i - z4] =
+          make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // Stores the float4 `v` at output position i0 of band `b` plus its image in
+  // the extension region for a consumer needing `halo` extension samples.
+  // The extension repeats with period len (reference src/wavelet.c:248-269:
+  // periodic src[t % len], mirror src[len - 1 - t % len]), so a halo longer
+  // than the signal takes one image per period.
+  const auto put = [&](float *b, int i0, float4 v, int halo) {
+    reinterpret_cast<float4 *>(b)[i0 >> 2] = v;
+    if (ext == EXTENSION_TYPE_PERIODIC) {
+      for (int t = i0; t < halo; t += len) reinterpret_cast<float4 *>(b + len + t)[0] = v;
+    } else if (ext == EXTENSION_TYPE_MIRROR) {
+      const float4 r = make_float4(v.w, v.z, v.y, v.x);
+      for (int t = len - 4 - i0; t < halo; t += len)
+        reinterpret_cast<float4 *>(b + len + t)[0] = r;
+    }
+  };
+  const float4 *x4 = reinterpret_cast<const float4 *>(src + sig * len);
+  for (int q = threadIdx.x; q < len4; q += blockDim.x) put(band0, 4 * q, x4[q], ORDER - 1);
+  float *in = band0, *out = band1;
+  for (int l = 0; l < levels; l++) {
+    const int dil = 1 << l;
+    __syncthreads();  // input band and its extension complete
+    if (ext == EXTENSION_TYPE_CONSTANT) {
+      const float c = in[len - 1];
+      for (int t = threadIdx.x; t < (ORDER - 1) * dil; t += blockDim.x) in[len + t] = c;
+      __syncthreads();
+    }
+    const bool last = l == levels - 1;
+    const int next_halo = (ORDER - 1) * dil * 2;
+    float4 *hrow = reinterpret_cast<float4 *>(hi + (sig * levels + l) * len);
+    for (int q = threadIdx.x; q < len4; q += blockDim.x) {
+      const int i0 = 4 * q;
+      float sh[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
+      if (dil <= 2) {
+        constexpr int W = (4 + 2 * (ORDER - 1) + 3) / 4;
+        float w[4 * W];
+#pragma unroll
+        for (int c = 0; c < W; c++) {
+          const float4 v = reinterpret_cast<const float4 *>(in + i0)[c];
+          w[4 * c] = v.x;
+          w[4 * c + 1] = v.y;
+          w[4 * c + 2] = v.z;
+          w[4 * c + 3] = v.w;
+        }
+        if (dil == 1) {
+#pragma unroll
+          for (int r = 0; r < ORDER; r++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              sh[e] = fmaf(hp[r], w[r + e], sh[e]);
+              sl[e] = fmaf(lp[r], w[r + e], sl[e]);
+            }
+        } else {
+#pragma unroll
+          for (int r = 0; r < ORDER; r++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              sh[e] = fmaf(hp[r], w[2 * r + e], sh[e]);
+              sl[e] = fmaf(lp[r], w[2 * r + e], sl[e]);
+            }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < ORDER; r++) {
+          const float4 v = *reinterpret_cast<const float4 *>(in + i0 + r * dil);
+          const float ve[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            sh[e] = fmaf(hp[r], ve[e], sh[e]);
+            sl[e] = fmaf(lp[r], ve[e], sl[e]);
+          }
+        }
+      }
+      const float4 hv = make_float4(sh[0], sh[1], sh[2], sh[3]);
+      const float4 lv = make_float4(sl[0], sl[1], sl[2], sl[3]);
+      if (NT) {
+        typedef float native4 __attribute__((ext_vector_type(4)));
+        const native4 nv = {hv.x, hv.y, hv.z, hv.w};
+        __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(hrow + q));
+      }
+      else
+        hrow[q] = hv;
+      if (last)
+        reinterpret_cast<float4 *>(lo + sig * len)[q] = lv;
+      else
+        put(out, i0, lv, next_halo);
+    }
+    float *t = in;
+    in = out;
+    out = t;
+  }
+}
+
+template <int ORDER>
+vs_status launch_swt_fused(const Taps &t, int ext, int levels, const float *src, int len,
+                           float *hi, float *lo, int batch, bool nt, hipStream_t s) {
+  const int halo = (ORDER - 1) << (levels - 1);
+  const size_t lds =
+      2 * static_cast<size_t>((len + halo + 2 * ORDER + 8 + 3) & ~3) * sizeof(float);
+  const void *fn = nt ? reinterpret_cast<const void *>(swt_fused_kernel<ORDER, true>)
+                      : reinterpret_cast<const void *>(swt_fused_kernel<ORDER, false>);
+  static const hipError_t attr0 = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(swt_fused_kernel<ORDER, false>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (kMultiMax + kMultiExt + 2 * 30 + 12) * 4);
+  static const hipError_t attr1 = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(swt_fused_kernel<ORDER, true>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (kMultiMax + kMultiExt + 2 * 30 + 12) * 4);
+  VS_HIP(attr0);
+  VS_HIP(attr1);
+  (void)fn;
+  if (nt)
+    hipLaunchKernelGGL((swt_fused_kernel<ORDER, true>), dim3(static_cast<unsigned>(batch)),
+                       dim3(256), lds, s, t, ext, levels, src, len, hi, lo);
+  else
+    hipLaunchKernelGGL((swt_fused_kernel<ORDER, false>), dim3(static_cast<unsigned>(batch)),
+                       dim3(256), lds, s, t, ext, levels, src, len, hi, lo);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+// Tuning knobs (vs_tune_set): "swt_fused" 0 = round-1 multi4 kernel,
+// 1 (default) = fused-extension kernel; "swt_nt" 1 (default) = non-temporal
+// hi stores (+3 % on db8 x 8 levels: the hi rows are never re-read here).
+int g_swt_fused = 1;
+int g_swt_nt = 1;
+
 template <int ORDER>
 vs_status launch_swt_multi4(const Taps &t, int ext, int levels, const float *src, int len,
                             float *hi, float *lo, int batch, hipStream_t s) {
@@ -431,6 +593,19 @@ vs_status make_taps(int type, int order, Taps *t) {
 }
 
 }  // namespace
+
+bool tune(const char *key, int value) {
+  if (std::strcmp(key, "swt_fused") == 0) {
+    g_swt_fused = value < 0 ? 1 : value;
+    return true;
+  }
+  if (std::strcmp(key, "swt_nt") == 0) {
+    g_swt_nt = value < 0 ? 1 : value;
+    return true;
+  }
+  return false;
+}
+
 }  // namespace wav
 }  // namespace vs
 
@@ -502,6 +677,17 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
   VS_TRY(make_taps(type, order, &t));
   auto s = static_cast<hipStream_t>(stream);
   const long long halo = static_cast<long long>(order - 1) << (levels - 1);
+  if (len <= kMultiMax && halo <= kMultiExt && len % 4 == 0 && g_swt_fused) {
+    const bool nt = g_swt_nt != 0;
+    switch (order) {
+#define VS_SWTF(O) \
+  case O: return launch_swt_fused<O>(t, ext, levels, src, len, hi, lo, batch, nt, s);
+      VS_SWTF(2) VS_SWTF(4) VS_SWTF(6) VS_SWTF(8) VS_SWTF(10) VS_SWTF(12) VS_SWTF(14)
+      VS_SWTF(16) VS_SWTF(18) VS_SWTF(20) VS_SWTF(24) VS_SWTF(30)
+#undef VS_SWTF
+      default: break;
+    }
+  }
   if (len <= kMultiMax && halo <= kMultiExt && len % 4 == 0) {
     switch (order) {
 #define VS_SWT4(O) \

@@ -219,3 +219,42 @@ def test_wavedec_long_signal_level_by_level(e):
         cur = nxt
         off += m
     np.testing.assert_allclose(pyr[:, off:], cur, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,o,levels,n", [(D, 8, 8, 1024), (S, 16, 6, 512), (D, 2, 10, 1024),
+                                          (C, 30, 5, 512), (D, 4, 9, 256)])
+@pytest.mark.parametrize("e", EXTS)
+@pytest.mark.parametrize("fused", [0, 1])
+def test_swt_multilevel_deep(t, o, levels, n, e, fused):
+    """vs_swt_multilevel at deep levels (halo up to the signal length, fused
+    extension kernel; (D, 4, 9, 256) has a halo longer than the signal and
+    still runs the fused kernel, one extension image per period) against the level-by-level host reference, with
+    the fused kernel on and off (vs_tune_set swt_fused)."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(o + 100 * levels + e)
+    b = 3
+    x = torch.randn(b, n, generator=g)
+    hi = torch.full((b, levels, n), float("nan"), device="cuda")
+    lo = torch.full((b, n), float("nan"), device="cuda")
+    xd = x.cuda()
+    assert lib.vs_tune_set(b"swt_fused", fused) == 0
+    try:
+        st = lib.vs_swt_multilevel(t, o, levels, e, ctypes.c_void_p(xd.data_ptr()), n,
+                                   ctypes.c_void_p(hi.data_ptr()), ctypes.c_void_p(lo.data_ptr()),
+                                   b, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert st == 0, lib.vs_last_error()
+        torch.cuda.synchronize()
+    finally:
+        lib.vs_tune_set(b"swt_fused", -1)
+    cur = x.numpy().copy()
+    for lvl in range(1, levels + 1):
+        for r in range(b):
+            vhi, vlo = capi.stationary_wavelet_apply(t, o, lvl, e, cur[r], na=True)
+            np.testing.assert_allclose(hi[r, lvl - 1].cpu().numpy(), vhi, atol=2e-4,
+                                       err_msg=f"level {lvl}")
+            cur[r] = vlo
+    np.testing.assert_allclose(lo.cpu().numpy(), cur, atol=2e-4)
