@@ -438,6 +438,116 @@ vs_status launch_swt_fused(const Taps &t, int ext, int levels, const float *src,
   return VS_OK;
 }
 
+// Signals longer than one workgroup's LDS (len > kMultiMax): tiles of
+// kTileOut outputs, each workgroup loading its tile plus the whole multi-level
+// support H = (ORDER-1)(2^L - 1) and running every level in LDS.  The band
+// of level l covers T + (ORDER-1)(2^L - 2^l) positions, so the last level
+// yields exactly the tile.  One HBM pass: read (1 + H/T) x, write L hi rows +
+// lo, instead of ~3 passes per level through HBM.
+// Positions past the end of the signal: periodic extension is exact by
+// circularity (computing a band from the periodic extension of its input gives
+// the periodic extension of the band); mirror / constant / zero are re-applied
+// to each band by the last tile, which starts at len - T so the mirrored
+// samples (the band's last H positions) are in its LDS.
+constexpr int kTileOut = 4096;
+
+template <int ORDER>
+__global__ __launch_bounds__(256) void swt_tiled_kernel(
+    Taps taps, int ext, int levels, const float *__restrict__ src, int len,
+    float *__restrict__ hi, float *__restrict__ lo) {
+  extern __shared__ __attribute__((aligned(16))) float smemt[];
+  const int H = (ORDER - 1) * ((1 << levels) - 1);
+  const int stride = (kTileOut + H + 2 * ORDER + 16 + 3) & ~3;
+  float *in = smemt, *out = smemt + stride;
+  const int64_t sig = blockIdx.y;
+  const int ntiles = gridDim.x;
+  const int t0 = static_cast<int>(blockIdx.x) == ntiles - 1 ? len - kTileOut
+                                                         : static_cast<int>(blockIdx.x) * kTileOut;
+  const bool tail = t0 + kTileOut + H > len;  // band reaches past the signal
+  float hp[ORDER], lp[ORDER];
+#pragma unroll
+  for (int r = 0; r < ORDER; r++) {
+    hp[r] = taps.hp[r];
+    lp[r] = taps.lp[r];
+  }
+  const float *x = src + sig * len;
+  for (int i = threadIdx.x; i < stride; i += blockDim.x) {
+    const int p = t0 + i;
+    in[i] = p < len ? x[p] : ext_load(x, p, len, ext);
+  }
+  for (int l = 0; l < levels; l++) {
+    const int dil = 1 << l;
+    const int nout = (kTileOut + (ORDER - 1) * ((1 << levels) - (2 << l)) + 3) & ~3;
+    __syncthreads();
+    float4 *hrow = reinterpret_cast<float4 *>(hi + (sig * levels + l) * len + t0);
+    const bool last = l == levels - 1;
+    for (int q = threadIdx.x; q < nout / 4; q += blockDim.x) {
+      const int i0 = 4 * q;
+      float sh[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < ORDER; r++) {
+        float ve[4];
+        if (dil >= 4) {
+          const float4 v = *reinterpret_cast<const float4 *>(in + i0 + r * dil);
+          ve[0] = v.x;
+          ve[1] = v.y;
+          ve[2] = v.z;
+          ve[3] = v.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++) ve[e] = in[i0 + r * dil + e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          sh[e] = fmaf(hp[r], ve[e], sh[e]);
+          sl[e] = fmaf(lp[r], ve[e], sl[e]);
+        }
+      }
+      const float4 lv = make_float4(sl[0], sl[1], sl[2], sl[3]);
+      if (i0 < kTileOut) {
+        typedef float native4 __attribute__((ext_vector_type(4)));
+        const native4 nv = {sh[0], sh[1], sh[2], sh[3]};
+        __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(hrow + q));
+        if (last) reinterpret_cast<float4 *>(lo + sig * len + t0)[q] = lv;
+      }
+      if (!last) reinterpret_cast<float4 *>(out)[q] = lv;
+    }
+    if (!last && tail && ext != EXTENSION_TYPE_PERIODIC) {
+      // re-extend the new band past the end of the signal from its own values
+      __syncthreads();
+      const int end = len - t0;  // local index of position len
+      for (int i = end + threadIdx.x; i < nout; i += blockDim.x) {
+        const int t = i - end;
+        float v = 0.f;
+        if (ext == EXTENSION_TYPE_MIRROR) v = out[end - 1 - (t % len)];
+        else if (ext == EXTENSION_TYPE_CONSTANT) v = out[end - 1];
+        out[i] = v;
+      }
+    }
+    float *tmp = in;
+    in = out;
+    out = tmp;
+  }
+}
+
+template <int ORDER>
+vs_status launch_swt_tiled(const Taps &t, int ext, int levels, const float *src, int len,
+                           float *hi, float *lo, int batch, hipStream_t s) {
+  const int H = (ORDER - 1) * ((1 << levels) - 1);
+  const size_t lds = 2 * static_cast<size_t>((kTileOut + H + 2 * ORDER + 16 + 3) & ~3) * 4;
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(swt_tiled_kernel<ORDER>),
+      hipFuncAttributeMaxDynamicSharedMemorySize,
+      2 * (kTileOut + kMultiExt + 2 * 30 + 16 + 3) * 4);
+  VS_HIP(attr);
+  const dim3 grid(static_cast<unsigned>((len + kTileOut - 1) / kTileOut),
+                  static_cast<unsigned>(batch));
+  hipLaunchKernelGGL(swt_tiled_kernel<ORDER>, grid, dim3(256), lds, s, t, ext, levels, src,
+                     len, hi, lo);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
 // Tuning knobs (vs_tune_set): "swt_fused" 0 = round-1 multi4 kernel,
 // 1 (default) = fused-extension kernel; "swt_nt" 1 (default) = non-temporal
 // hi stores (+3 % on db8 x 8 levels: the hi rows are never re-read here).
@@ -709,8 +819,21 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
     VS_HIP(hipGetLastError());
     return VS_OK;
   }
-  // Long signals: level by level through HBM (lo of level l feeds level
-  // l+1, ping-ponging between two scratch bands; the last level writes lo).
+  // Long signals: tiles with the whole multi-level support in LDS.
+  const long long support = static_cast<long long>(order - 1) * ((1LL << levels) - 1);
+  if (len > kMultiMax && len % 4 == 0 && support <= kMultiExt && batch <= kMaxGridY &&
+      g_swt_fused) {
+    switch (order) {
+#define VS_SWTT(O) \
+  case O: return launch_swt_tiled<O>(t, ext, levels, src, len, hi, lo, batch, s);
+      VS_SWTT(2) VS_SWTT(4) VS_SWTT(6) VS_SWTT(8) VS_SWTT(10) VS_SWTT(12) VS_SWTT(14)
+      VS_SWTT(16) VS_SWTT(18) VS_SWTT(20) VS_SWTT(24) VS_SWTT(30)
+#undef VS_SWTT
+      default: break;
+    }
+  }
+  // Otherwise level by level through HBM (lo of level l feeds level l+1,
+  // ping-ponging between two scratch bands; the last level writes lo).
   if (batch > kMaxGridY)
     return batch_chunks(batch, [&](long long b0, int nb) {
       return vs_swt_multilevel(type, order, levels, ext, src + b0 * len, len,

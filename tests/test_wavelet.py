@@ -258,3 +258,48 @@ def test_swt_multilevel_deep(t, o, levels, n, e, fused):
                                        err_msg=f"level {lvl}")
             cur[r] = vlo
     np.testing.assert_allclose(lo.cpu().numpy(), cur, atol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,o,levels,n", [(D, 8, 8, 12000), (S, 4, 3, 40000), (C, 30, 7, 9000),
+                                          (D, 2, 12, 16384)])
+@pytest.mark.parametrize("e", EXTS)
+def test_swt_multilevel_long_tiled(t, o, levels, n, e):
+    """Signals longer than one workgroup's LDS (> 8192 samples): tiled
+    all-levels-in-LDS kernel (wavelet.hip swt_tiled_kernel; the last tile is
+    aligned to the end of the signal and re-extends each band) against the
+    level-by-level host reference and the HBM level-by-level path."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(o + levels + e + n)
+    b = 2
+    x = torch.randn(b, n, generator=g)
+    xd = x.cuda()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for fused in (1, 0):
+        hi = torch.full((b, levels, n), float("nan"), device="cuda")
+        lo = torch.full((b, n), float("nan"), device="cuda")
+        assert lib.vs_tune_set(b"swt_fused", fused) == 0
+        try:
+            st = lib.vs_swt_multilevel(t, o, levels, e, ctypes.c_void_p(xd.data_ptr()), n,
+                                       ctypes.c_void_p(hi.data_ptr()),
+                                       ctypes.c_void_p(lo.data_ptr()), b, s)
+            assert st == 0, lib.vs_last_error()
+            torch.cuda.synchronize()
+        finally:
+            lib.vs_tune_set(b"swt_fused", -1)
+        outs.append((hi.cpu(), lo.cpu()))
+    torch.testing.assert_close(outs[0][0], outs[1][0], atol=1e-4, rtol=0)
+    torch.testing.assert_close(outs[0][1], outs[1][1], atol=1e-4, rtol=0)
+    hi, lo = outs[0]
+    cur = x.numpy().copy()
+    for lvl in range(1, levels + 1):
+        for r in range(b):
+            vhi, vlo = capi.stationary_wavelet_apply(t, o, lvl, e, cur[r], na=True)
+            np.testing.assert_allclose(hi[r, lvl - 1].numpy(), vhi, atol=3e-4,
+                                       err_msg=f"level {lvl}")
+            cur[r] = vlo
+    np.testing.assert_allclose(lo.numpy(), cur, atol=3e-4)
