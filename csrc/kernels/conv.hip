@@ -23,6 +23,7 @@
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 
@@ -801,8 +802,17 @@ __global__ __launch_bounds__(256) void spectrum_mul_kernel(
 }  // namespace
 
 // Tuning knob (vs_tune_set("os_block_log_max", n)): cap of the overlap-save
-// block size, for A/B measurements.
-int g_os_log_max = fft::kMaxLdsLog;
+// block size, for A/B measurements.  The real-block kernel reaches one more
+// power of two than the complex transforms (L = 2M real samples).
+int g_os_log_max = fft::kMaxLdsLog + 1;
+// Tuning knob (vs_tune_set("os_block_extra", 0/2/3/4)): overlap-save block
+// L = 2^(floor(log2 h) + extra); the reference uses 2 (src/convolve.c:116-121).
+// 0 (default): 3 while that keeps L <= 8192, else 2 -- the M <= 4096 real
+// kernels run ~1.25x more block points per second than the M = 8192 one
+// (x = 2^20 x 64, Msamples/s, profiles/r2/conv_block_rule.md):
+//   h = 700: 344 -> 388 K, 1000: 260 -> 336 K, 2000: 270 -> 330 K;
+//   h = 3000 / 4096 keep L = 8192 / 16384 (L = 16384 / 32768: -7 % / -14 %).
+int g_os_extra = 0;
 // Tuning knob (vs_tune_set("conv_buffer", 0/1)): buffer-descriptor loads and
 // stores in the fused block kernels.
 int g_conv_buf = 1;
@@ -814,16 +824,24 @@ int g_conv_real = 1;
 // every block size (default: L >= 8192 only, see use_real).
 int g_conv_real_all = 0;
 
+bool use_real(int logl);
+
+// Largest single-workgroup block: the real-block kernel transforms L = 2M
+// real samples as an M-point complex FFT, so it reaches 2^(kMaxLdsLog + 1).
+int max_block_log() { return use_real(fft::kMaxLdsLog + 1) ? fft::kMaxLdsLog + 1 : fft::kMaxLdsLog; }
+
 int os_block_log(int hlen) {
   // Reference block size 2^(floor(log2 M) + 2) (src/convolve.c:116-121),
   // raised to >= 2048 so every block amortises its transform over >= ~75%
   // useful outputs, capped at the single-workgroup LDS transform.
-  int lg = 2;
+  int lg = g_os_extra ? g_os_extra : 3;
   int m = hlen;
   while (m >>= 1) lg++;
+  if (g_os_extra == 0 && lg > 13) lg--;
   if (lg < 11) lg = 11;
-  if (lg > g_os_log_max) lg = g_os_log_max;
-  while ((1 << lg) <= hlen && lg < fft::kMaxLdsLog) lg++;  // must exceed h - 1
+  const int cap = std::min(g_os_log_max, max_block_log());
+  if (lg > cap) lg = cap;
+  while ((1 << lg) <= hlen && lg < cap) lg++;  // must exceed h - 1
   return lg;
 }
 
@@ -838,7 +856,7 @@ int select(int xlen, int hlen, int batch) {
   const bool os_ok = (1 << los) - (hlen - 1) >= (1 << los) / 2;  // >= 50% useful
   int lm = 1;
   while ((1LL << lm) < ylen) lm++;
-  if (lm <= fft::kMaxLdsLog && (!os_ok || ylen <= (1LL << los)))
+  if (lm <= max_block_log() && (!os_ok || ylen <= (1LL << los)))
     return VS_CONV_FFT;  // one block covers the whole output
   if (os_ok) return VS_CONV_OVERLAP_SAVE;
   // Long filter: one padded transform while it exists, else partitioned
@@ -957,7 +975,7 @@ vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, i
     logl = kRealMinLog;
     while ((1LL << logl) < ylen) logl++;
   }
-  VS_REQUIRE(logl >= kRealMinLog && logl <= fft::kMaxLdsLog,
+  VS_REQUIRE(logl >= kRealMinLog && logl <= fft::kMaxLdsLog + 1,
              "real-block convolution: block 2^%d out of range", logl);
   const int L = 1 << logl;
   RealArgs a{};
@@ -989,6 +1007,8 @@ vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, i
       if (g_conv_real == 2)
         return run_real_t<13, 16>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
       return run_real_t<13, 32>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
+    case 14:
+      return run_real_t<14, 0>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
   }
   set_error("real-block convolution: unsupported block 2^%d", logl);
   return VS_ERR_UNSUPPORTED;
@@ -1168,8 +1188,13 @@ int vs_conv1d_os_block(int hlen) { return 1 << conv::os_block_log(hlen); }
 vs_status vs_tune_set(const char *key, int value) {
   VS_REQUIRE(key, "vs_tune_set: null key");
   if (std::strcmp(key, "os_block_log_max") == 0) {
-    VS_REQUIRE(value >= 4 && value <= fft::kMaxLdsLog, "os_block_log_max out of range");
+    VS_REQUIRE(value >= 4 && value <= fft::kMaxLdsLog + 1, "os_block_log_max out of range");
     conv::g_os_log_max = value;
+    return VS_OK;
+  }
+  if (std::strcmp(key, "os_block_extra") == 0) {
+    VS_REQUIRE(value == 0 || (value >= 2 && value <= 4), "os_block_extra must be 0 or 2..4");
+    conv::g_os_extra = value;
     return VS_OK;
   }
   if (std::strcmp(key, "conv_buffer") == 0) {
@@ -1225,7 +1250,7 @@ vs_status vs_conv1d(int algo, int correlate, const float *x, int xlen,
           (hlen + conv::kPartTaps - 1) / conv::kPartTaps);
       return conv::run_partitioned(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
     case VS_CONV_FFT:
-      if (lm <= fft::kMaxLdsLog) {
+      if (lm <= fft::kMaxLdsLog || (lm == fft::kMaxLdsLog + 1 && conv::use_real(lm))) {
         if (conv::use_real(lm))
           return conv::run_real(correlate, false, x, xlen, xs, h, hlen, hs, y, ys,
                                 static_cast<int>(ylen), static_cast<int>(ylen), 0, batch, s);

@@ -91,7 +91,9 @@ def test_per_signal_filters_real_block():
 @pytest.mark.parametrize("xlen,hlen,batch", [(300000, 9000, 2), (200001, 12345, 1)])
 @pytest.mark.parametrize("corr", [False, True])
 def test_partitioned_long_filters(xlen, hlen, batch, corr):
-    """Filters longer than one overlap-save block: explicit OS request."""
+    """Filters of 9000-12345 taps, explicit OS request: one L = 32768 real
+    block since round 2 (partitions before; test_partitioned_beyond_32768_block
+    keeps the partitioned path covered)."""
     _check(xlen, hlen, batch, "overlap_save", corr)
 
 
@@ -158,3 +160,29 @@ def test_direct_large_grid(hlen):
     least two workgroups per CU, filters over one 512-tap LDS chunk too."""
     _check(300000, hlen, 4, "direct", False, rel=1e-6)
     _check(300000, hlen, 4, "direct", True, rel=1e-6)
+
+
+@pytest.mark.parametrize("xlen,hlen,batch", [(1 << 17, 4096, 3), (100003, 3000, 2),
+                                             (70001, 700, 2), (40000, 8191, 1)])
+@pytest.mark.parametrize("corr", [False, True])
+def test_overlap_save_block_extra3(xlen, hlen, batch, corr):
+    """os_block_extra = 3: blocks of 2^(floor(log2 h) + 3), up to L = 32768
+    real samples (real_conv_kernel<14>: a 16384-point complex transform,
+    128 KiB LDS)."""
+    with _knob("os_block_extra", 3, 0):
+        _check(xlen, hlen, batch, "overlap_save", corr)
+
+
+@pytest.mark.parametrize("xlen,hlen", [(300000, 16000), (20000, 12000)])
+def test_real_block_32768_default(xlen, hlen):
+    """Filters of 8192..16383 taps: one L = 32768 real block (was a 50 %-useful
+    16384 block or partitions), and a single-block FFT of 2^15 points."""
+    _check(xlen, hlen, 2, "overlap_save", False)
+    _check(xlen, hlen, 2, "overlap_save", True)
+    _check(12000, 9000, 2, "fft", False)
+
+
+def test_partitioned_beyond_32768_block():
+    """Filters longer than the largest real block still partition."""
+    _check(200000, 40000, 1, "overlap_save", False)
+    _check(200000, 40000, 1, "overlap_save", True)

@@ -17,7 +17,7 @@ from veles.simd_amd import _lib  # noqa: E402
 
 lib = _lib.lib()
 lib.vs_tune_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
-DEFAULTS = {"conv_buffer": 1, "conv_real": 1, "conv_real_all": 0}
+DEFAULTS = {"conv_buffer": 1, "conv_real": 1, "conv_real_all": 0, "os_block_extra": 0}
 
 
 def main():
@@ -33,11 +33,11 @@ def main():
         ylen = xlen + hlen - 1
         y = torch.empty(batch, ylen, device="cuda")
         knobs = [kv.split("=") for kv in os.environ.get("KNOBS", "").split(",") if kv]
-        variants = [("auto", 0, 14, {})]
+        variants = [("auto", 0, 15, {})]
         for name, vals in knobs:
-            variants += [(f"{name}={v}", 0, 14, {name: int(v)}) for v in vals.split("/")]
+            variants += [(f"{name}={v}", 0, 15, {name: int(v)}) for v in vals.split("/")]
         if not knobs:
-            variants += [("direct", 1, 14, {}), ("fft", 2, 14, {})]
+            variants += [("direct", 1, 15, {}), ("fft", 2, 15, {})]
             variants += [(f"os{lg}", 3, lg, {}) for lg in (11, 12, 13, 14)
                          if (1 << lg) > 2 * hlen + 64]
         times = {v[0]: [] for v in variants}
@@ -66,7 +66,7 @@ def main():
                 times[name].append(ev0.elapsed_time(ev1) / reps)
                 for k in kn:  # back to the library defaults
                     lib.vs_tune_set(k.encode(), DEFAULTS.get(k, 1))
-        lib.vs_tune_set(b"os_block_log_max", 14)
+        lib.vs_tune_set(b"os_block_log_max", 15)
         out = {k: round(xlen * batch / statistics.median(v) / 1e3, 1) for k, v in times.items()}
         res[hlen] = out
         print(f"h={hlen}: Msamples/s", out, flush=True)
