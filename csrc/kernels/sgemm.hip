@@ -7,7 +7,9 @@
 // and two-stage generations are in git history, profiles/r1/sgemm_variants.md):
 //   * gen 5 (sgemm5_kernel): NN, whole 256 x 256 tiles -- a three-stage
 //     LDS-DMA ring, hand-pipelined so the barrier sits mid-tile and the next
-//     tile's fragment reads interleave with this tile's MFMAs;
+//     tile's fragment reads interleave with this tile's MFMAs; the default
+//     runs 8 waves (2 x 4, two per SIMD, 128 x 64 per wave) so one wave's
+//     barrier and LDS waits are covered by the other's MFMAs;
 //   * gen 6 (sgemm6_kernel): the same pipeline for every transpose, ragged
 //     M / N / K and any alignment, with 256 x 256, 128 x 128 and 64 x 64
 //     tiles and split-K for shapes with few output tiles.
@@ -746,7 +748,11 @@ bool launch_gen6(const GemmArgs &g0, int ta, int tb, int batch, hipStream_t s, i
   return true;
 }
 
-using Cfg5D = Cfg5<256, 256, 2, 2, 0, true>;  // 4 waves of 128 x 128, AGPR accumulators
+using Cfg5D = Cfg5<256, 256, 2, 2, 0, true>;
+// 8-wave gen-5 tiles (two waves per SIMD: one wave's barrier / LDS waits
+// are filled by the other's MFMAs; 128 accumulator AGPRs per wave)
+using Cfg5W24 = Cfg5<256, 256, 2, 4, 0, true>;
+using Cfg5W42 = Cfg5<256, 256, 4, 2, 0, true>;  // 4 waves of 128 x 128, AGPR accumulators
 
 __global__ __launch_bounds__(256) void scale_c_kernel(int m, int n, float beta,
                                                       float *__restrict__ c, int64_t ldc,
@@ -798,11 +804,12 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
   if (variant < 0) {
     // Largest tile that still gives every CU work (interleaved A/B on
     // MI355X against hipBLASLt: profiles/r2/sgemm_gen6_ab.md): 256 x 256
-    // tiles from 256 of them (gen 5 for NN whole tiles, gen 6 otherwise),
+    // tiles from 256 of them (8-wave gen 5 for NN whole tiles -- +2-3 % over
+    // the 4-wave one, profiles/r2/sgemm_w8_ab.md -- gen 6 otherwise),
     // 128 x 128 from 256, else 64 x 64 with split-K.
     const long t256 = static_cast<long>((m + 255) / 256) * ((n + 255) / 256) * batch;
     const long t128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
-    if (t256 >= 256) variant = 3;
+    if (t256 >= 256) variant = 6;
     else if (t128 >= 256) variant = 1;
     else variant = 4;
   }
@@ -817,6 +824,14 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
       break;
     case 4: ok = launch_gen6(g, ta, tb, batch, s, 2); break;      // 64 x 64, split-K
     case 5: ok = launch_gen6(g, ta, tb, batch, s, 0); break;      // 128 x 128, split-K
+    case 6:  // gen 5 NN with 8 waves (2 x 4, two per SIMD), else 256 x 256
+      ok = launch_cfg5<Cfg5W24>(g, ta, tb, gen6_dma16(g, ta, tb, batch), batch, s) ||
+           launch_gen6(g, ta, tb, batch, s, 1, 1);
+      break;
+    case 7:  // gen 5 NN with 8 waves (4 x 2), else 256 x 256
+      ok = launch_cfg5<Cfg5W42>(g, ta, tb, gen6_dma16(g, ta, tb, batch), batch, s) ||
+           launch_gen6(g, ta, tb, batch, s, 1, 1);
+      break;
     default:
       set_error("vs_sgemm: unknown variant %d (0..%d)", variant, VS_SGEMM_VARIANTS - 1);
       return VS_ERR_INVALID;
