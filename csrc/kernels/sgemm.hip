@@ -698,11 +698,14 @@ bool gen6_dma16(const GemmArgs &g, int ta, int tb, int batch) {
 }
 
 // tile: 0 = 128 x 128 (4 waves of 64 x 64), 1 = 256 x 256 (4 waves of
-// 128 x 128, AGPR accumulators), 2 = 64 x 64 (4 waves of 32 x 32); 4-byte
-// DMA at 128 x 128 / 64 x 64 only (vmcnt range).
+// 128 x 128, AGPR accumulators), 2 = 64 x 64 (4 waves of 32 x 32),
+// 3 / 4 = 256 x 256 with 8 waves (2 x 4 / 4 x 2, two per SIMD); 4-byte DMA
+// at 128 x 128 / 64 x 64 only (vmcnt range).
 bool launch_gen6_tile(const GemmArgs &g, int ta, int tb, int batch, hipStream_t s, int tile) {
   const bool d16 = gen6_dma16(g, ta, tb, batch);
   if (tile == 1 && d16) return launch_gen6_t<256, 256, 2, 2, 16, true, 0>(g, ta, tb, batch, s);
+  if (tile == 3 && d16) return launch_gen6_t<256, 256, 2, 4, 16, true, 0>(g, ta, tb, batch, s);
+  if (tile == 4 && d16) return launch_gen6_t<256, 256, 4, 2, 16, true, 0>(g, ta, tb, batch, s);
   if (tile == 2) {
     if (d16) return launch_gen6_t<64, 64, 2, 2, 16, false, 0>(g, ta, tb, batch, s);
     return launch_gen6_t<64, 64, 2, 2, 4, false, 0>(g, ta, tb, batch, s);
@@ -716,7 +719,7 @@ bool launch_gen6_tile(const GemmArgs &g, int ta, int tb, int batch, hipStream_t 
 // partial tiles to a workspace, one reduction pass applying alpha / beta.
 bool launch_gen6(const GemmArgs &g0, int ta, int tb, int batch, hipStream_t s, int tile,
                  int splits = 0) {
-  const int bm = tile == 1 ? 256 : tile == 2 ? 64 : 128;
+  const int bm = (tile == 1 || tile == 3 || tile == 4) ? 256 : tile == 2 ? 64 : 128;
   const long tiles = static_cast<long>((g0.m + bm - 1) / bm) * ((g0.n + bm - 1) / bm) * batch;
   if (splits <= 0) {
     const long want = 2L * device_cu_count();
@@ -824,13 +827,13 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
       break;
     case 4: ok = launch_gen6(g, ta, tb, batch, s, 2); break;      // 64 x 64, split-K
     case 5: ok = launch_gen6(g, ta, tb, batch, s, 0); break;      // 128 x 128, split-K
-    case 6:  // gen 5 NN with 8 waves (2 x 4, two per SIMD), else 256 x 256
+    case 6:  // 256 x 256 with 8 waves (2 x 4, two per SIMD): gen 5 NN, else gen 6
       ok = launch_cfg5<Cfg5W24>(g, ta, tb, gen6_dma16(g, ta, tb, batch), batch, s) ||
-           launch_gen6(g, ta, tb, batch, s, 1, 1);
+           launch_gen6(g, ta, tb, batch, s, 3, 1);
       break;
-    case 7:  // gen 5 NN with 8 waves (4 x 2), else 256 x 256
+    case 7:  // 256 x 256 with 8 waves (4 x 2): gen 5 NN, else gen 6
       ok = launch_cfg5<Cfg5W42>(g, ta, tb, gen6_dma16(g, ta, tb, batch), batch, s) ||
-           launch_gen6(g, ta, tb, batch, s, 1, 1);
+           launch_gen6(g, ta, tb, batch, s, 4, 1);
       break;
     default:
       set_error("vs_sgemm: unknown variant %d (0..%d)", variant, VS_SGEMM_VARIANTS - 1);
