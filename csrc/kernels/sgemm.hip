@@ -699,13 +699,18 @@ bool gen6_dma16(const GemmArgs &g, int ta, int tb, int batch) {
 
 // tile: 0 = 128 x 128 (4 waves of 64 x 64), 1 = 256 x 256 (4 waves of
 // 128 x 128, AGPR accumulators), 2 = 64 x 64 (4 waves of 32 x 32),
-// 3 / 4 = 256 x 256 with 8 waves (2 x 4 / 4 x 2, two per SIMD); 4-byte DMA
+// 3 / 4 = 256 x 256 with 8 waves (2 x 4 / 4 x 2, two per SIMD), 5 = 128 x 128
+// with 8 waves (2 x 4); 4-byte DMA
 // at 128 x 128 / 64 x 64 only (vmcnt range).
 bool launch_gen6_tile(const GemmArgs &g, int ta, int tb, int batch, hipStream_t s, int tile) {
   const bool d16 = gen6_dma16(g, ta, tb, batch);
   if (tile == 1 && d16) return launch_gen6_t<256, 256, 2, 2, 16, true, 0>(g, ta, tb, batch, s);
   if (tile == 3 && d16) return launch_gen6_t<256, 256, 2, 4, 16, true, 0>(g, ta, tb, batch, s);
   if (tile == 4 && d16) return launch_gen6_t<256, 256, 4, 2, 16, true, 0>(g, ta, tb, batch, s);
+  if (tile == 5) {  // 128 x 128 with 8 waves (2 x 4 of 64 x 32)
+    if (d16) return launch_gen6_t<128, 128, 2, 4, 16, false, 0>(g, ta, tb, batch, s);
+    return launch_gen6_t<128, 128, 2, 4, 4, false, 0>(g, ta, tb, batch, s);
+  }
   if (tile == 2) {
     if (d16) return launch_gen6_t<64, 64, 2, 2, 16, false, 0>(g, ta, tb, batch, s);
     return launch_gen6_t<64, 64, 2, 2, 4, false, 0>(g, ta, tb, batch, s);
@@ -714,18 +719,23 @@ bool launch_gen6_tile(const GemmArgs &g, int ta, int tb, int batch, hipStream_t 
   return launch_gen6_t<128, 128, 2, 2, 4, false, 0>(g, ta, tb, batch, s);
 }
 
+// Split-K count for `tiles` output tiles: k slices of >= 256 until
+// tiles x slices reaches ~2 per CU.
+int auto_splits(long tiles, int k) {
+  const long want = 2L * device_cu_count();
+  int splits = 1;
+  while (tiles * splits * 2 <= want && k / (splits * 2) >= 256) splits *= 2;
+  return splits;
+}
+
 // Gen 6 with split-K when the output tiles cannot fill the chip: k slices
 // of >= 256 (a multiple of 16) until tiles x slices reaches ~2 per CU,
 // partial tiles to a workspace, one reduction pass applying alpha / beta.
 bool launch_gen6(const GemmArgs &g0, int ta, int tb, int batch, hipStream_t s, int tile,
                  int splits = 0) {
-  const int bm = (tile == 1 || tile == 3 || tile == 4) ? 256 : tile == 2 ? 64 : 128;
+  const int bm = (tile == 1 || tile == 3 || tile == 4) ? 256 : tile == 2 ? 64 : 128;  // 0, 5: 128
   const long tiles = static_cast<long>((g0.m + bm - 1) / bm) * ((g0.n + bm - 1) / bm) * batch;
-  if (splits <= 0) {
-    const long want = 2L * device_cu_count();
-    splits = 1;
-    while (tiles * splits * 2 <= want && g0.k / (splits * 2) >= 256) splits *= 2;
-  }
+  if (splits <= 0) splits = auto_splits(tiles, g0.k);
   if (splits <= 1) {
     GemmArgs g = g0;
     g.kchunk = 0;
@@ -778,6 +788,33 @@ int default_variant() {
   return v;
 }
 
+// Default kernel choice: for each candidate (tile, workgroups per CU,
+// relative per-CU throughput), the split-K count launch_gen6 would use and
+// the wave-quantisation efficiency of tiles x splits over CUs x slots; the
+// best modelled score wins, larger tiles on ties.  Calibrated on MI355X
+// (profiles/r2/sgemm_w8_ab.md): 256 x 256 8-wave 1 / CU at 1.0, 128 x 128
+// 8-wave 2 / CU at 0.94, 64 x 64 4-wave 4 / CU at 0.90, split-K passes x 0.95.
+// E.g. 4096^3 -> 256 tiles (143 TF); 3072^3 -> 64 x 64 (125 vs 103 TF with
+// 128 x 128); 2048 x 4096 x 2048 -> 128 x 128; 1024 x 1024 x 4096 -> 128 x 128
+// split-K (97 vs 90 TF).
+int pick_variant(int m, int n, int k, int batch) {
+  const long cus = device_cu_count();
+  const auto eff = [&](long work, long slots) {
+    const long waves = (work + slots - 1) / slots;
+    return static_cast<double>(work) / static_cast<double>(waves * slots);
+  };
+  const long t256 = static_cast<long>((m + 255) / 256) * ((n + 255) / 256) * batch;
+  const long t128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
+  const long t64 = static_cast<long>((m + 63) / 64) * ((n + 63) / 64) * batch;
+  const int s128 = auto_splits(t128, k), s64 = auto_splits(t64, k);
+  const double a = eff(t256, cus);
+  const double b = 0.94 * eff(t128 * s128, 2 * cus) * (s128 > 1 ? 0.95 : 1.0);
+  const double c = 0.90 * eff(t64 * s64, 4 * cus) * (s64 > 1 ? 0.95 : 1.0);
+  if (a >= b && a >= c) return 6;
+  if (b >= c) return s128 > 1 ? 9 : 8;
+  return 4;
+}
+
 vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
                      float alpha, const float *a, int64_t lda, int64_t sa,
                      const float *b, int64_t ldb, int64_t sb, float beta,
@@ -804,18 +841,7 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
   }
   GemmArgs g{m, n, k, alpha, beta, a, lda, sa, b, ldb, sb, c, ldc, sc, 0, 0};
   if (variant < 0) variant = default_variant();
-  if (variant < 0) {
-    // Largest tile that still gives every CU work (interleaved A/B on
-    // MI355X against hipBLASLt: profiles/r2/sgemm_gen6_ab.md): 256 x 256
-    // tiles from 256 of them (8-wave gen 5 for NN whole tiles -- +2-3 % over
-    // the 4-wave one, profiles/r2/sgemm_w8_ab.md -- gen 6 otherwise),
-    // 128 x 128 from 256, else 64 x 64 with split-K.
-    const long t256 = static_cast<long>((m + 255) / 256) * ((n + 255) / 256) * batch;
-    const long t128 = static_cast<long>((m + 127) / 128) * ((n + 127) / 128) * batch;
-    if (t256 >= 256) variant = 6;
-    else if (t128 >= 256) variant = 1;
-    else variant = 4;
-  }
+  if (variant < 0) variant = pick_variant(m, n, k, batch);
   bool ok = false;
   switch (variant) {
     case 0: ok = launch_gen6(g, ta, tb, batch, s, 2, 1); break;   // 64 x 64
@@ -835,6 +861,8 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
       ok = launch_cfg5<Cfg5W42>(g, ta, tb, gen6_dma16(g, ta, tb, batch), batch, s) ||
            launch_gen6(g, ta, tb, batch, s, 4, 1);
       break;
+    case 8: ok = launch_gen6(g, ta, tb, batch, s, 5, 1); break;  // 128 x 128, 8 waves
+    case 9: ok = launch_gen6(g, ta, tb, batch, s, 5); break;     // same, split-K
     default:
       set_error("vs_sgemm: unknown variant %d (0..%d)", variant, VS_SGEMM_VARIANTS - 1);
       return VS_ERR_INVALID;

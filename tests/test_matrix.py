@@ -146,7 +146,7 @@ def test_sgemm_autograd():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", list(range(8)))
+@pytest.mark.parametrize("variant", list(range(10)))
 def test_sgemm_every_variant(variant):
     """Every SGEMM kernel variant (include/simd/gpu.h VS_SGEMM_VARIANTS) on
     an aligned NN shape (gen 5's shape) and on ragged / transposed shapes,
