@@ -564,7 +564,7 @@ __device__ __forceinline__ void real_spectrum_chunk(float2 (&v)[PL::E], const fl
   for (int c = 0; c < CN; c++) {
     const int e = C0 + c;
     const int k = reg_index<PL, RL>(t, e / RL, e % RL);
-    const float2 zm = lds[fft::lds_slot((PL::N - k) & (PL::N - 1))];
+    const float2 zm = lds[fft::slot<PL>((PL::N - k) & (PL::N - 1))];
     v[e] = fft::cadd(cmul(make_float2(pq[c].x, pq[c].y), v[e]),
                      fft::cmulc(make_float2(pq[c].z, pq[c].w), zm));
   }
@@ -592,7 +592,7 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS)) void real_conv_kernel(
   using PL = Plan<LOGM, EP>;
   constexpr int E = PL::E;
   constexpr int CH = E / 4;  // P / Q chunk (elements)
-  __shared__ float2 lds[PL::N];
+  __shared__ float2 lds[PL::kLds];
   const int t = threadIdx.x;
   // grid = (blocks per signal, signals): both indices stay in SGPRs (a
   // buffer descriptor built from a VALU-divided index turned every load
@@ -625,7 +625,7 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS)) void real_conv_kernel(
   for (int b = 0; b < E / RL; b++)
 #pragma unroll
     for (int j = 0; j < RL; j++)
-      lds[fft::lds_slot(reg_index<PL, RL>(t, b, j))] = v[b * RL + j];
+      lds[fft::slot<PL>(reg_index<PL, RL>(t, b, j))] = v[b * RL + j];
   fft::lds_barrier();
   real_pq_load<PL, CH, CH>(PQ, t, pq1);
   __builtin_amdgcn_sched_barrier(0);
@@ -684,7 +684,7 @@ __global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
     const float2 *__restrict__ tw, const float2 *__restrict__ twl, float4 *__restrict__ PQ) {
   using PL = Plan<LOGM>;
   constexpr int E = PL::E;
-  __shared__ float2 lds[PL::N];
+  __shared__ float2 lds[PL::kLds];
   const int t = threadIdx.x;
   const float *hr = h + static_cast<long long>(blockIdx.x) * hs;
   constexpr int R0 = PL::first_radix(false);
@@ -704,7 +704,7 @@ __global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
   __builtin_amdgcn_sched_barrier(0);
   fft::transform<PL, false, false>(v, lds, t, twf);
 #pragma unroll
-  for (int e = 0; e < E; e++) lds[fft::lds_slot(reg_index<PL, RL>(t, e / RL, e % RL))] = v[e];
+  for (int e = 0; e < E; e++) lds[fft::slot<PL>(reg_index<PL, RL>(t, e / RL, e % RL))] = v[e];
   fft::lds_barrier();
   float4 *out = PQ + static_cast<long long>(blockIdx.x) * PL::N;
   const float sc = 1.0f / static_cast<float>(PL::N);
@@ -712,7 +712,7 @@ __global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
   for (int e = 0; e < E; e++) {
     const int k = reg_index<PL, RL>(t, e / RL, e % RL);
     const float2 zk = v[e];
-    const float2 zm = lds[fft::lds_slot((PL::N - k) & (PL::N - 1))];
+    const float2 zm = lds[fft::slot<PL>((PL::N - k) & (PL::N - 1))];
     const float2 w = wk[e];                    // W^k, W = exp(-2 pi i / L)
     const float2 iw = make_float2(-w.y, w.x);  // i W^k
     const float2 ca = make_float2(0.5f * (1.f - iw.x), -0.5f * iw.y);

@@ -280,10 +280,20 @@ struct Plan {
   static constexpr bool R32 = E == 32;
   static constexpr int NPASS =
       R32 ? (LOGN + 4) / 5 : (LOGN >= 4 ? LOGN / 4 + (SMALL ? 1 : 0) : 1);
+  // LDS layout of the exchanges.  32-point plans pad one element per 32
+  // (slot e + e / 32): every element a thread exchanges then sits at its
+  // base slot plus a compile-time offset (ds_read / ds_write immediates, no
+  // per-access address VALU -- the XOR swizzle cost ~1000 of the 3787 VALU
+  // instructions per wave of the M = 8192 conv kernel) and every pass pattern
+  // stays bank-conflict-free.  Other plans keep the XOR swizzle (lds_slot).
+  // 16-point plans of >= 1024 points pad one element per 16 (the pass
+  // patterns of radix-16 butterflies stay conflict-free at that period).
+  static constexpr int PADLOG = E == 32 ? 5 : (E == 16 && LOGN >= 10 ? 4 : 0);
+  static constexpr bool PAD = PADLOG != 0;
   // per-signal LDS (float2).  Signals narrower than a 32-lane read group
   // (TPS < 32, several per wave) are TPS slots apart so their aligned
   // TPS-slot read blocks land in different banks.
-  static constexpr int kLds = N + (TPS < 32 ? TPS : 0);
+  static constexpr int kLds = PAD ? N + (N >> PADLOG) : N + (TPS < 32 ? TPS : 0);
   // Radix of pass q (forward order: the odd radix first).
   static constexpr int radix(int q) {
     if (R32) return q == 0 ? (1 << (LOGN - 5 * (NPASS - 1))) : 32;
@@ -300,6 +310,13 @@ struct Plan {
     return rev ? radix_rev(NPASS - 1) : radix(NPASS - 1);
   }
 };
+
+// LDS slot of element e under plan PL's layout.
+template <class PL>
+__device__ __forceinline__ int slot(int e) {
+  if constexpr (PL::PAD) return e + (e >> PL::PADLOG);
+  else return lds_slot(e);
+}
 
 // Pass Q of a transform (REV: radices in reverse order).  On entry v holds
 // this pass's inputs (butterfly b: i = t + b TPS, v[b R + j] = x[i + j N/R]);
@@ -350,8 +367,21 @@ struct Pass {
           const int i = t + b * PL::TPS;
           const int k = i & (P - 1);
           const int base = (i - k) * R + k;
+          if constexpr (PL::PAD) {
+            constexpr int G = 1 << PL::PADLOG;
+            static_assert(P == 1 || (R * P) % G == 0, "padded layout: carry-free offsets");
+            // base % G + (j P) % G < G for every pass (P = 1: base is a multiple
+            // of R > j; else R P is a multiple of G, so base % G = k < P and
+            // (j P) % G is a multiple of the power of two P), hence
+            // slot(base + j P) = slot(base) + j P + (j P) / G
+            const int sb = base + (base >> PL::PADLOG);
 #pragma unroll
-          for (int j = 0; j < R; j++) lds[lds_slot(base + j * P)] = comp(v[b * R + j]);
+            for (int j = 0; j < R; j++)
+              lds[sb + j * P + ((j * P) >> PL::PADLOG)] = comp(v[b * R + j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < R; j++) lds[lds_slot(base + j * P)] = comp(v[b * R + j]);
+          }
         }
       };
       // LDS -> the next pass's inputs, element e of v via `sink(e, value)`
@@ -359,8 +389,16 @@ struct Pass {
 #pragma unroll
         for (int b = 0; b < PL::E / R2; b++) {
           const int i = t + b * PL::TPS;
+          if constexpr (PL::PAD) {
+            static_assert((PL::N / R2) % (1 << PL::PADLOG) == 0, "padded layout: read stride");
+            constexpr int D = PL::N / R2 + ((PL::N / R2) >> PL::PADLOG);
+            const int si = i + (i >> PL::PADLOG);
 #pragma unroll
-          for (int j = 0; j < R2; j++) sink(b * R2 + j, lds[lds_slot(i + j * (PL::N / R2))]);
+            for (int j = 0; j < R2; j++) sink(b * R2 + j, lds[si + j * D]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < R2; j++) sink(b * R2 + j, lds[lds_slot(i + j * (PL::N / R2))]);
+          }
         }
       };
       put([](float2 z) { return z; });
