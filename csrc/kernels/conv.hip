@@ -521,37 +521,44 @@ __device__ __forceinline__ void store_real(const RealArgs &a, float *yr, int st,
   constexpr int R0 = PL::radix(0);  // last pass of the reversed-radix inverse
   // valid block positions [lo, hi): history dropped, row end respected
   const int lo = a.pre, hi = min(a.pre + a.step, a.ylen - st);
-  const auto w = __builtin_amdgcn_make_buffer_rsrc(yr, 0, BUF ? 4 * a.yroom : 0, 0x00020000);
+  if constexpr (BUF) {
+    // The descriptor covers exactly the valid outputs [st + lo, st + hi):
+    // history positions get negative offsets (as unsigned: past the range)
+    // and are dropped by the buffer unit -- no per-element compares or
+    // branches.  lo is even (run_real), so no pair straddles the start; a
+    // pair straddling the row end keeps its in-range first dword (range
+    // check per dword; tests: odd / even filter and row lengths).
+    const auto w = __builtin_amdgcn_make_buffer_rsrc(yr + st + lo, 0, 4 * max(hi - lo, 0),
+                                                     0x00020000);
 #pragma unroll
-  for (int b = 0; b < PL::E / R0; b++)
+    for (int b = 0; b < PL::E / R0; b++)
 #pragma unroll
-    for (int j = 0; j < R0; j++) {
-      const int p = 2 * reg_index<PL, R0>(t, b, j);
-      float2 r = v[b * R0 + j];
-      const bool ok0 = p >= lo && p < hi, ok1 = p + 1 >= lo && p + 1 < hi;
-      if constexpr (BUF) {
-        const int off = 4 * (st + p);
-        if (ok0 && ok1) {
-          if (a.accumulate) {
-            const auto o = __builtin_amdgcn_raw_buffer_load_b64(w, off, 0, 0);
-            r.x += __uint_as_float(o[0]);
-            r.y += __uint_as_float(o[1]);
-          }
-          __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(r.x),
-                                                             __float_as_uint(r.y)};
-          __builtin_amdgcn_raw_buffer_store_b64(u, w, off, 0, 0);
-        } else if (ok0 || ok1) {
-          const int o1 = ok0 ? off : off + 4;
-          float q = ok0 ? r.x : r.y;
-          if (a.accumulate) q += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(w, o1, 0, 0));
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(q), w, o1, 0, 0);
+      for (int j = 0; j < R0; j++) {
+        const int p = 2 * reg_index<PL, R0>(t, b, j);
+        float2 r = v[b * R0 + j];
+        const int off = 4 * (p - lo);
+        if (a.accumulate) {
+          const auto o = __builtin_amdgcn_raw_buffer_load_b64(w, off, 0, 0);
+          r.x += __uint_as_float(o[0]);
+          r.y += __uint_as_float(o[1]);
         }
-      } else {
+        __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(r.x),
+                                                           __float_as_uint(r.y)};
+        __builtin_amdgcn_raw_buffer_store_b64(u, w, off, 0, 0);
+      }
+  } else {
+#pragma unroll
+    for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+      for (int j = 0; j < R0; j++) {
+        const int p = 2 * reg_index<PL, R0>(t, b, j);
+        const float2 r = v[b * R0 + j];
+        const bool ok0 = p >= lo && p < hi, ok1 = p + 1 >= lo && p + 1 < hi;
         float *dst = yr + st + p;
         if (ok0) dst[0] = a.accumulate ? dst[0] + r.x : r.x;
         if (ok1) dst[1] = a.accumulate ? dst[1] + r.y : r.y;
       }
-    }
+  }
 }
 
 // Spectrum step of real_conv_kernel on elements [C0, C0 + CN) of v (pattern
@@ -987,7 +994,12 @@ vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, i
   a.ylen = ylen;
   a.yroom = yroom;
   a.pq_per_signal = hs != 0;
-  a.pre = overlap_save ? hlen - 1 : 0;
+  // history of at least h - 1 samples, rounded up to even: every block's
+  // first valid output then starts a sample pair, which store_real's
+  // descriptor-range stores need (a b64 store whose first dword lies before
+  // the range is dropped whole -- measured: odd h - 1 lost each block's
+  // first output)
+  a.pre = overlap_save ? (hlen - 1 + 1) & ~1 : 0;
   a.step = L - a.pre;
   VS_REQUIRE(a.step > 0 && hlen <= L, "real-block convolution: filter (%d) longer than the block (%d)",
              hlen, L);
