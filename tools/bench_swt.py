@@ -46,14 +46,15 @@ def main():
     lo = torch.empty(nsig, n, device="cuda")
     nbytes = 4 * nsig * n * (levels + 2)
     res = {}
-    # ceilings on the same volume
-    wbuf = torch.empty(nbytes // 4, device="cuda")
-    half = torch.empty(nbytes // 8, device="cuda")
-    half2 = torch.empty_like(half)
-    fill = statistics.median(timed(lambda: wbuf.fill_(1.0), 5) for _ in range(rounds))
-    copy = statistics.median(timed(lambda: half2.copy_(half), 5) for _ in range(rounds))
-    res["ceiling_fill_TBps"] = round(nbytes / fill / 1e12, 2)
-    res["ceiling_copy_TBps"] = round(nbytes / copy / 1e12, 2)
+    # ceilings on the same volume (NO_CEIL=1 skips them)
+    wbuf = torch.empty(nbytes // 4, device="cuda") if os.environ.get("NO_CEIL") != "1" else None
+    half = torch.empty(nbytes // 8, device="cuda") if wbuf is not None else None
+    half2 = torch.empty_like(half) if wbuf is not None else None
+    if wbuf is not None:
+        fill = statistics.median(timed(lambda: wbuf.fill_(1.0), 5) for _ in range(rounds))
+        copy = statistics.median(timed(lambda: half2.copy_(half), 5) for _ in range(rounds))
+        res["ceiling_fill_TBps"] = round(nbytes / fill / 1e12, 2)
+        res["ceiling_copy_TBps"] = round(nbytes / copy / 1e12, 2)
     del wbuf, half, half2
     for order in orders:
         ref = None
