@@ -347,8 +347,10 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
 
 template <class C>
 vs_status launch_glds(const Args &g, int batch, hipStream_t s) {
-  VS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_glds_kernel<C>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes));
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&gemm_glds_kernel<C>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);  // once per instantiation
+  VS_HIP(attr);
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
   hipLaunchKernelGGL((gemm_glds_kernel<C>), dim3(tiles, 1, static_cast<unsigned>(batch)),

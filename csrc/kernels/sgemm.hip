@@ -309,8 +309,11 @@ __global__ __launch_bounds__(C::kThreads) void sgemm5_kernel(GemmArgs g) {
 template <class C>
 bool launch_cfg5(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipStream_t s) {
   if (ta || tb || !vec || g.m % C::BM || g.n % C::BN || g.k % C::BK || g.k == 0) return false;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&sgemm5_kernel<C>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);
+  // once per instantiation (a runtime call per launch shows in host-API timings)
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&sgemm5_kernel<C>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);
+  (void)attr;
   const unsigned tiles = static_cast<unsigned>((g.m / C::BM) * (g.n / C::BN));
   hipLaunchKernelGGL(sgemm5_kernel<C>, dim3(tiles, 1, static_cast<unsigned>(batch)),
                      dim3(C::kThreads), C::kLdsBytes, s, g);
@@ -651,8 +654,10 @@ bool gen6_fits(const GemmArgs &g) {
 template <class C>
 bool launch_cfg6(const GemmArgs &g, int batch, hipStream_t s) {
   if (!gen6_fits<C>(g)) return false;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&sgemm6_kernel<C>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&sgemm6_kernel<C>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);
+  (void)attr;
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
   const unsigned splits = g.kchunk ? static_cast<unsigned>((g.k + g.kchunk - 1) / g.kchunk) : 1;
