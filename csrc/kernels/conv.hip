@@ -860,7 +860,13 @@ int select(int xlen, int hlen, int batch) {
   // (405 vs 267 Gsamples/s, profiles/r1/conv_sweep_v2.log).
   if (ylen <= 64 || hlen <= 8 || (hlen <= 32 && xlen < 4096)) return VS_CONV_DIRECT;
   const int los = os_block_log(hlen);
-  const bool os_ok = (1 << los) - (hlen - 1) >= (1 << los) / 2;  // >= 50% useful
+  // Overlap-save while >= 15 % of each block is useful output: the block rule
+  // keeps >= 75 % up to h = 8192; past that L = 32768 real blocks still beat
+  // the whole-signal four-step FFT (~45 Gsamples/s at 2^20 x 64) down to
+  // ~12 % useful -- h = 20000 (39 %): 144 vs 45; h = 30000 (8 %): 36 vs 45
+  // (profiles/r2/conv/conv_long.log).
+  const bool os_ok = static_cast<long long>((1 << los) - (hlen - 1)) * 100 >=
+                     15LL * (1 << los);
   int lm = 1;
   while ((1LL << lm) < ylen) lm++;
   if (lm <= max_block_log() && (!os_ok || ylen <= (1LL << los)))

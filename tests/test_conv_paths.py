@@ -116,7 +116,9 @@ def test_four_step_fft_conv_2p23():
     """x + h - 1 just above 2^22 -> a 2^23-point four-step transform."""
     from veles.simd_amd import _lib
     xlen, hlen = (1 << 22) + 4096 - 20000 + 1, 20000
-    assert _lib.lib().vs_conv1d_select(xlen, hlen, 1) == 2
+    # auto picks overlap-save here (L = 32768 blocks, 39 % useful, since the
+    # 15 % rule); the explicit FFT request below still runs the 2^23 transform
+    assert _lib.lib().vs_conv1d_select(xlen, hlen, 1) == 3
     _check(xlen, hlen, 1, "fft", False)
     _check(xlen, hlen, 1, "fft", True)
 
@@ -186,3 +188,15 @@ def test_partitioned_beyond_32768_block():
     """Filters longer than the largest real block still partition."""
     _check(200000, 40000, 1, "overlap_save", False)
     _check(200000, 40000, 1, "overlap_save", True)
+
+
+def test_select_long_filter_overlap_save():
+    """Filters whose L = 32768 block is >= 15 % useful run overlap-save
+    (h = 20000: 144 vs 45 Gsamples/s for the four-step FFT); shorter blocks
+    fall back to the FFT (profiles/r2/conv/conv_long.log)."""
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    assert lib.vs_conv1d_select(1 << 20, 20000, 64) == 3
+    assert lib.vs_conv1d_select(1 << 20, 30000, 64) == 2
+    _check(200000, 20000, 2, "auto", False)
+    _check(200000, 20000, 1, "auto", True)

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Conv1d throughput sweep (Msamples/s of input) over algorithms, filter
 lengths and overlap-save block caps, interleaved in one process.
+SKIP_DIRECT=1 drops the direct arm (long filters); "os" is an explicit
+overlap-save request (single block up to L = 32768, else partitions).
 KNOBS="name=v0/v1,..." adds A/B arms of vs_tune_set knobs on the auto path
 (e.g. KNOBS="conv_buffer=0/1"); every arm is checked against
 the first one."""
@@ -37,7 +39,9 @@ def main():
         for name, vals in knobs:
             variants += [(f"{name}={v}", 0, 15, {name: int(v)}) for v in vals.split("/")]
         if not knobs:
-            variants += [("direct", 1, 15, {}), ("fft", 2, 15, {})]
+            if os.environ.get("SKIP_DIRECT") != "1":
+                variants += [("direct", 1, 15, {})]
+            variants += [("fft", 2, 15, {}), ("os", 3, 15, {})]
             variants += [(f"os{lg}", 3, lg, {}) for lg in (11, 12, 13, 14)
                          if (1 << lg) > 2 * hlen + 64]
         times = {v[0]: [] for v in variants}
