@@ -593,8 +593,16 @@ __device__ __forceinline__ void real_pq_load(const float4 *__restrict__ PQ, int 
 // chunks one chunk ahead of the products, the inverse twiddles before the
 // spectrum exchange -- TableTw / plain indexing waited for each L2 hit
 // right before its use (32 serial P / Q round trips per block).
+// Waves per SIMD the compiler must allow for (VGPR budget 512 / waves): the
+// 16-point M = 8192 plan runs 8 waves per workgroup, so two workgroups per CU
+// (16 waves) need <= 128 VGPRs.
+template <int LOGM, int EP>
+constexpr int real_min_waves() {
+  return Plan<LOGM, EP>::TPS >= 512 && Plan<LOGM, EP>::E == 16 ? 4 : 1;
+}
+
 template <int LOGM, int EP, bool BUF>
-__global__ __launch_bounds__((Plan<LOGM, EP>::TPS)) void real_conv_kernel(
+__global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())) void real_conv_kernel(
     RealArgs a, const float2 *__restrict__ tw) {
   using PL = Plan<LOGM, EP>;
   constexpr int E = PL::E;
