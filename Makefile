@@ -100,7 +100,7 @@ docs:
 # Host AddressSanitizer build of the library + native C API test (host code
 # only: device ASan / XNACK is not available on the GPU pool).  Runs the
 # host-reference paths on any machine: `make asan && ASAN_OPTIONS=detect_leaks=1 \
-#   build-asan/tests/capi_test --host`.
+#   VELES_DISABLE_GPU=1 build-asan/tests/capi_test`.
 ASAN_BUILD := build-asan
 ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer
 asan:
