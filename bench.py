@@ -154,6 +154,22 @@ def main():
         csteps = max(5, args.steps // 2)
         dtc = _timed(conv_step, csteps, max(2, args.warmup // 2), dist_on)
         msamples = CONV_LEN * CONV_BATCH * csteps * world / dtc / 1e6
+        # Same convolution through a vs_conv1d plan (filter spectra computed
+        # once at plan creation, outside the timed loop -- the fixed-filter
+        # FIR / serving use; the number above recomputes them every call).
+        plan = ctypes.c_void_p()
+        if lib.vs_conv1d_plan_create(0, 0, CONV_LEN, ph, CONV_H, 0, 1, ctypes.byref(plan),
+                                     stream) == 0:
+            def plan_step():
+                st = lib.vs_conv1d_plan_execute(plan, px, CONV_LEN, py, ylen, CONV_BATCH,
+                                                stream)
+                if st:
+                    raise RuntimeError(lib.vs_last_error().decode())
+            dtp = _timed(plan_step, csteps, max(2, args.warmup // 2), dist_on)
+            torch.cuda.synchronize()
+            lib.vs_conv1d_plan_destroy(plan)
+            secondary["conv1d_plan_msamples_per_s"] = round(
+                CONV_LEN * CONV_BATCH * csteps * world / dtp / 1e6, 1)
         secondary.update({
             "conv1d_msamples_per_s": round(msamples, 1),
             "conv1d_ms_per_step": round(dtc / csteps * 1e3, 3),

@@ -744,21 +744,39 @@ __global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
   }
 }
 
-template <int LOGM, int EP>
-vs_status run_real_t(int correlate, const float *h, int hlen, int64_t hs, int nfilt,
-                     RealArgs a, long long nblocks, hipStream_t s) {
-  using PL = Plan<LOGM, EP>;
+// P / Q of nfilt filters (stride hs) for the L = 2^(LOGM+1) real block into
+// `pq` (PL::N float4 per filter).
+template <int LOGM>
+vs_status launch_real_filter(int correlate, const float *h, int hlen, int64_t hs, int nfilt,
+                             float4 *pq, hipStream_t s) {
   vs_status st;
   const float2 *tw = fft::twiddles(LOGM, &st);
   if (!tw) return st;
   const float2 *twl = fft::twiddles(LOGM + 1, &st);
   if (!twl) return st;
-  DeviceBuffer pq;
-  VS_TRY(pq.alloc(sizeof(float4) * PL::N * static_cast<size_t>(nfilt), s));
   hipLaunchKernelGGL((real_filter_kernel<LOGM>), dim3(static_cast<unsigned>(nfilt)),
-                     dim3(Plan<LOGM>::TPS), 0, s, h, hlen, hs, correlate, tw, twl,
-                     pq.as<float4>());
-  a.PQ = pq.as<float4>();
+                     dim3(Plan<LOGM>::TPS), 0, s, h, hlen, hs, correlate, tw, twl, pq);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
+// One real-block convolution pass: the filter spectra (unless `pq_pre`
+// already holds them -- a vs_conv1d plan) then the block kernel.
+template <int LOGM, int EP>
+vs_status run_real_t(int correlate, const float *h, int hlen, int64_t hs, int nfilt,
+                     RealArgs a, long long nblocks, const float4 *pq_pre, hipStream_t s) {
+  using PL = Plan<LOGM, EP>;
+  vs_status st;
+  const float2 *tw = fft::twiddles(LOGM, &st);
+  if (!tw) return st;
+  DeviceBuffer pq;
+  if (pq_pre) {
+    a.PQ = pq_pre;
+  } else {
+    VS_TRY(pq.alloc(sizeof(float4) * PL::N * static_cast<size_t>(nfilt), s));
+    VS_TRY(launch_real_filter<LOGM>(correlate, h, hlen, hs, nfilt, pq.as<float4>(), s));
+    a.PQ = pq.as<float4>();
+  }
   const dim3 grid(static_cast<unsigned>(a.nblk), static_cast<unsigned>(nblocks / a.nblk));
   if (g_conv_buf && a.xlen < (1 << 29) && a.yroom < (1 << 29))
     hipLaunchKernelGGL((real_conv_kernel<LOGM, EP, true>), grid, dim3(PL::TPS), 0, s, a, tw);
@@ -988,7 +1006,8 @@ bool use_real(int logl) {
 // per row from y); accumulate adds them to what is there.
 vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, int64_t xs,
                    const float *h, int hlen, int64_t hs, float *y, int64_t ys, int ylen,
-                   int yroom, int accumulate, int batch, hipStream_t s) {
+                   int yroom, int accumulate, int batch, hipStream_t s,
+                   const float4 *pq_pre = nullptr) {
   int logl;
   if (overlap_save) {
     logl = os_block_log(hlen);
@@ -1025,16 +1044,16 @@ vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, i
   const int nfilt = hs ? batch : 1;
   switch (logl - 1) {
 #define VS_CASE(LG, EP) \
-  case LG: return run_real_t<LG, EP>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
+  case LG: return run_real_t<LG, EP>(correlate, h, hlen, hs, nfilt, a, nblocks, pq_pre, s);
     VS_CASE(6, 0) VS_CASE(7, 0) VS_CASE(8, 0) VS_CASE(9, 0) VS_CASE(10, 0) VS_CASE(11, 0)
     VS_CASE(12, 0)
 #undef VS_CASE
     case 13:
       if (g_conv_real == 2)
-        return run_real_t<13, 16>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
-      return run_real_t<13, 32>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
+        return run_real_t<13, 16>(correlate, h, hlen, hs, nfilt, a, nblocks, pq_pre, s);
+      return run_real_t<13, 32>(correlate, h, hlen, hs, nfilt, a, nblocks, pq_pre, s);
     case 14:
-      return run_real_t<14, 0>(correlate, h, hlen, hs, nfilt, a, nblocks, s);
+      return run_real_t<14, 0>(correlate, h, hlen, hs, nfilt, a, nblocks, pq_pre, s);
   }
   set_error("real-block convolution: unsupported block 2^%d", logl);
   return VS_ERR_UNSUPPORTED;
@@ -1210,6 +1229,128 @@ int vs_conv1d_select(int xlen, int hlen, int batch) {
 }
 
 int vs_conv1d_os_block(int hlen) { return 1 << conv::os_block_log(hlen); }
+
+}  // extern "C"
+
+struct vs_conv_plan {
+  int algo, correlate, xlen, hlen, nfilt;
+  bool overlap_save;  // real plans: overlap-save blocks vs one block
+  float4 *pq;         // real plans: nfilt x 2^(logl-1) P / Q entries
+  float *h;           // other plans: nfilt x hlen taps
+};
+
+extern "C" {
+
+vs_status vs_conv1d_plan_create(int algo, int correlate, int xlen, const float *h, int hlen,
+                                int64_t hs, int nfilt, vs_conv_plan **plan,
+                                vs_stream_t stream) {
+  VS_REQUIRE(plan && h, "vs_conv1d_plan_create: null pointer");
+  *plan = nullptr;
+  VS_REQUIRE(xlen > 0 && hlen > 0 && nfilt >= 1, "vs_conv1d_plan_create: empty shape");
+  VS_REQUIRE(nfilt == 1 || hs >= hlen, "vs_conv1d_plan_create: filter stride < filter length");
+  const long long ylen = static_cast<long long>(xlen) + hlen - 1;
+  VS_REQUIRE(ylen < (1LL << 31), "vs_conv1d_plan_create: output too long");
+  auto s = static_cast<hipStream_t>(stream);
+  if (algo == VS_CONV_AUTO) algo = conv::select(xlen, hlen, nfilt);
+  VS_REQUIRE(algo >= VS_CONV_DIRECT && algo <= VS_CONV_OVERLAP_SAVE,
+             "vs_conv1d_plan_create: unknown algorithm %d", algo);
+  // The real-block path vs_conv1d would take for this shape, if any
+  int logl = 0;
+  bool os = false;
+  if (algo == VS_CONV_OVERLAP_SAVE) {
+    const int l = conv::os_block_log(hlen);
+    if ((1 << l) > hlen - 1 + 16 && conv::use_real(l)) logl = l, os = true;
+  } else if (algo == VS_CONV_FFT) {
+    int lm = 1;
+    while ((1LL << lm) < ylen) lm++;
+    if (lm <= fft::kMaxLdsLog + 1 && conv::use_real(lm)) {
+      logl = conv::kRealMinLog;
+      while ((1LL << logl) < ylen) logl++;
+    }
+  }
+  auto *p = new vs_conv_plan{algo, correlate, xlen, hlen, nfilt, os, nullptr, nullptr};
+  vs_status st = VS_OK;
+  if (logl) {
+    const size_t n = (static_cast<size_t>(1) << (logl - 1)) * nfilt;
+    if (hipMalloc(&p->pq, n * sizeof(float4)) != hipSuccess) {
+      (void)hipGetLastError();
+      st = VS_ERR_ALLOC;
+      set_error("vs_conv1d_plan_create: out of device memory (%zu B)", n * sizeof(float4));
+    } else {
+      switch (logl - 1) {
+#define VS_CASE(LG)                                                                           \
+  case LG:                                                                                    \
+    st = conv::launch_real_filter<LG>(correlate, h, hlen, nfilt > 1 ? hs : 0, nfilt, p->pq, s); \
+    break;
+        VS_CASE(6) VS_CASE(7) VS_CASE(8) VS_CASE(9) VS_CASE(10) VS_CASE(11) VS_CASE(12)
+        VS_CASE(13) VS_CASE(14)
+#undef VS_CASE
+        default:
+          st = VS_ERR_UNSUPPORTED;
+          set_error("vs_conv1d_plan_create: unsupported block 2^%d", logl);
+      }
+    }
+  } else {
+    const size_t n = static_cast<size_t>(hlen) * nfilt;
+    if (hipMalloc(&p->h, n * sizeof(float)) != hipSuccess) {
+      (void)hipGetLastError();
+      st = VS_ERR_ALLOC;
+      set_error("vs_conv1d_plan_create: out of device memory (%zu B)", n * sizeof(float));
+    } else if (hipMemcpy2DAsync(p->h, hlen * sizeof(float), h,
+                                (nfilt > 1 ? hs : hlen) * sizeof(float), hlen * sizeof(float),
+                                nfilt, hipMemcpyDefault, s) != hipSuccess) {
+      (void)hipGetLastError();
+      st = VS_ERR_HIP;
+      set_error("vs_conv1d_plan_create: filter copy failed");
+    }
+  }
+  if (st != VS_OK) {
+    vs_conv1d_plan_destroy(p);
+    return st;
+  }
+  *plan = p;
+  return VS_OK;
+}
+
+vs_status vs_conv1d_plan_execute(const vs_conv_plan *p, const float *x, int64_t xs, float *y,
+                                 int64_t ys, int batch, vs_stream_t stream) {
+  VS_REQUIRE(p && x && y, "vs_conv1d_plan_execute: null pointer");
+  VS_REQUIRE(batch >= 0, "vs_conv1d_plan_execute: negative batch");
+  VS_REQUIRE(p->nfilt == 1 || batch == p->nfilt,
+             "vs_conv1d_plan_execute: plan has %d per-signal filters, batch %d", p->nfilt,
+             batch);
+  if (batch == 0) return VS_OK;
+  const int ylen = p->xlen + p->hlen - 1;
+  VS_REQUIRE(batch <= 1 || (xs >= p->xlen && ys >= ylen),
+             "vs_conv1d_plan_execute: row strides smaller than the rows");
+  auto s = static_cast<hipStream_t>(stream);
+  if (!p->pq)
+    return vs_conv1d(p->algo, p->correlate, x, p->xlen, xs, p->h, p->hlen,
+                     p->nfilt > 1 ? p->hlen : 0, y, ys, batch, stream);
+  if (batch > kMaxGridY) {
+    VS_REQUIRE(p->nfilt == 1, "vs_conv1d_plan_execute: per-signal batch > %lld", kMaxGridY);
+    return batch_chunks(batch, [&](long long b0, int nb) {
+      return vs_conv1d_plan_execute(p, x + b0 * xs, xs, y + b0 * ys, ys, nb, stream);
+    });
+  }
+  // h is not read when the spectra are precomputed; hs only flags per-signal P / Q
+  return conv::run_real(p->correlate, p->overlap_save, x, p->xlen, xs, nullptr, p->hlen,
+                        p->nfilt > 1 ? p->hlen : 0, y, ys, ylen, ylen, 0, batch, s, p->pq);
+}
+
+vs_status vs_conv1d_plan_info(const vs_conv_plan *p, int *algo, int *precomputed) {
+  VS_REQUIRE(p, "vs_conv1d_plan_info: null plan");
+  if (algo) *algo = p->algo;
+  if (precomputed) *precomputed = p->pq ? 1 : 0;
+  return VS_OK;
+}
+
+void vs_conv1d_plan_destroy(vs_conv_plan *p) {
+  if (!p) return;
+  if (p->pq) (void)hipFree(p->pq);
+  if (p->h) (void)hipFree(p->h);
+  delete p;
+}
 
 vs_status vs_tune_set(const char *key, int value) {
   VS_REQUIRE(key, "vs_tune_set: null key");

@@ -216,6 +216,27 @@ vs_status vs_conv1d(int algo, int correlate, const float *x, int x_len,
 int vs_conv1d_select(int x_len, int h_len, int batch);
 /// Overlap-save block length the library uses for filter length h_len.
 int vs_conv1d_os_block(int h_len);
+
+/// Convolution plan: fixed filter(s) and signal length, many executions
+/// (FIR filters, matched filters at inference).  Creation resolves the
+/// algorithm and, on the real-block FFT / overlap-save paths, computes the
+/// filter spectra once (the per-call vs_conv1d recomputes them: ~13 us for a
+/// 4096-tap filter); other paths keep a device copy of the taps and run
+/// vs_conv1d.  h: n_filters rows of h_len taps, row stride h_stride (device
+/// pointer; copied / transformed during creation, on `stream`).
+/// n_filters = 1 (shared filter, any batch) or the batch (one per signal).
+typedef struct vs_conv_plan vs_conv_plan;
+vs_status vs_conv1d_plan_create(int algo, int correlate, int x_len, const float *h,
+                                int h_len, int64_t h_stride, int n_filters,
+                                vs_conv_plan **plan, vs_stream_t stream);
+/// y[b] = x[b] (*) h of the plan; the same contract as vs_conv1d.
+vs_status vs_conv1d_plan_execute(const vs_conv_plan *plan, const float *x,
+                                 int64_t x_stride, float *y, int64_t y_stride,
+                                 int batch, vs_stream_t stream);
+/// Resolved algorithm and whether the filter spectra are precomputed.
+vs_status vs_conv1d_plan_info(const vs_conv_plan *plan, int *algo, int *precomputed);
+/// Frees the plan (after the streams that used it are done with it).
+void vs_conv1d_plan_destroy(vs_conv_plan *plan);
 /// Tuning knobs for measurements ("os_block_log_max": cap of the
 /// overlap-save block, log2).
 vs_status vs_tune_set(const char *key, int value);

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Conv1d throughput sweep (Msamples/s of input) over algorithms, filter
 lengths and overlap-save block caps, interleaved in one process.
+PLAN=1 adds a vs_conv1d_plan arm (filter spectra computed once);
 SKIP_DIRECT=1 drops the direct arm (long filters); "os" is an explicit
 overlap-save request (single block up to L = 32768, else partitions).
 KNOBS="name=v0/v1,..." adds A/B arms of vs_tune_set knobs on the auto path
@@ -44,6 +45,12 @@ def main():
             variants += [("fft", 2, 15, {}), ("os", 3, 15, {})]
             variants += [(f"os{lg}", 3, lg, {}) for lg in (11, 12, 13, 14)
                          if (1 << lg) > 2 * hlen + 64]
+        plan = None
+        if os.environ.get("PLAN") == "1":   # vs_conv1d_plan: filter spectra precomputed
+            plan = ctypes.c_void_p()
+            assert lib.vs_conv1d_plan_create(0, 0, xlen, h.data_ptr(), hlen, 0, 1,
+                                             ctypes.byref(plan), s) == 0, lib.vs_last_error()
+            variants.append(("plan", 0, 15, {}))
         times = {v[0]: [] for v in variants}
         ev0, ev1 = torch.cuda.Event(True), torch.cuda.Event(True)
         ref = None
@@ -52,8 +59,13 @@ def main():
                 lib.vs_tune_set(b"os_block_log_max", lg)
                 for k, v in kn.items():
                     lib.vs_tune_set(k.encode(), v)
-                run = lambda: lib.vs_conv1d(algo, 0, x.data_ptr(), xlen, xlen, h.data_ptr(),
-                                            hlen, 0, y.data_ptr(), ylen, batch, s)
+                if name == "plan":
+                    run = lambda: lib.vs_conv1d_plan_execute(plan, x.data_ptr(), xlen,
+                                                             y.data_ptr(), ylen, batch, s)
+                else:
+                    run = lambda: lib.vs_conv1d(algo, 0, x.data_ptr(), xlen, xlen,
+                                                h.data_ptr(), hlen, 0, y.data_ptr(), ylen,
+                                                batch, s)
                 assert run() == 0, lib.vs_last_error()
                 if r == 0:
                     if ref is None:

@@ -32,8 +32,23 @@ class FIRFilter(nn.Module):
         self.mode = mode
         self.algorithm = algorithm
 
+    def _planned(self, x: torch.Tensor):
+        """Inference with fixed taps on the GPU: a cached Conv1dPlan (filter
+        spectra computed once) keyed by signal length, device and the taps'
+        version counter; None when autograd or the CPU path applies."""
+        if (not x.is_cuda or x.dtype != torch.float32 or self.taps.requires_grad
+                and torch.is_grad_enabled()):
+            return None
+        key = (x.shape[-1], x.device, self.taps._version, self.taps.data_ptr())
+        if getattr(self, "_plan_key", None) != key:
+            self._plan = ops.Conv1dPlan(self.taps.detach().to(x.device), x.shape[-1],
+                                        self.algorithm)
+            self._plan_key = key
+        return self._plan
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = ops.conv1d(x, self.taps, self.algorithm)
+        plan = self._planned(x)
+        y = plan(x) if plan is not None else ops.conv1d(x, self.taps, self.algorithm)
         H = self.taps.shape[-1]
         X = x.shape[-1]
         if self.mode == "same":

@@ -11,7 +11,7 @@ from .elementwise import (add, affine, binary, complex_conjugate,  # noqa: F401
                           complex_multiply, convert, cos, exp, log, math,
                           minmax, mul, normalize2d, pow, saxpy, sin, sincos, sqrt, sub,
                           sum_all)
-from .signal import (conv1d, conv1d_algorithm, correlate, detect_peaks,  # noqa: F401
+from .signal import (Conv1dPlan, conv1d, conv1d_algorithm, correlate, detect_peaks,  # noqa: F401
                      dwt, fft, irfft, rfft, swt, swt_level, wavedec,
                      wavelet_filter)
 
@@ -19,6 +19,6 @@ __all__ = [
     "sgemm", "sgemm_bf16x3", "gemm_bf16", "matmul", "matmul_transposed", "convert", "binary", "add", "sub",
     "mul", "complex_multiply", "complex_conjugate", "affine", "saxpy", "math",
     "sin", "cos", "log", "exp", "sum_all", "minmax", "normalize2d", "conv1d",
-    "correlate", "conv1d_algorithm", "fft", "rfft", "irfft", "dwt", "swt",
+    "correlate", "conv1d_algorithm", "Conv1dPlan", "fft", "rfft", "irfft", "dwt", "swt",
     "wavedec", "wavelet_filter", "detect_peaks", "swt_level",
 ]

@@ -7,6 +7,8 @@ CPU tensors run an fp64-accumulated torch reference of the same math.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from .. import _lib
@@ -61,6 +63,60 @@ def _conv1d(x: torch.Tensor, h: torch.Tensor, algorithm: int,
 @_conv1d.register_fake
 def _(x, h, algorithm, correlate):
     return x.new_empty((*x.shape[:-1], x.shape[-1] + h.shape[-1] - 1))
+
+
+class Conv1dPlan:
+    """Fixed filter(s) and signal length, many executions on the GPU
+    (vs_conv1d_plan_*): the algorithm is resolved and, on the real-block
+    FFT / overlap-save paths, the filter spectra are computed once at
+    creation instead of at every call.  The taps are copied / transformed at
+    creation, so later changes to `h` do not affect the plan.
+
+    plan = Conv1dPlan(h, x_len); y = plan(x)   # x: [..., x_len] float32 cuda
+    h: [h_len] (shared) or [batch, h_len] (one filter per signal).
+    """
+
+    def __init__(self, h: torch.Tensor, x_len: int, algorithm="auto",
+                 correlate: bool = False):
+        if not h.is_cuda or h.dtype != torch.float32:
+            raise TypeError("Conv1dPlan: float32 cuda filter expected")
+        hr = h.reshape(-1, h.shape[-1]).contiguous()
+        self.x_len, self.h_len, self.n_filters = int(x_len), hr.shape[1], hr.shape[0]
+        self.correlate = bool(correlate)
+        self.device = h.device
+        self._plan = ctypes.c_void_p()
+        with on_device(h):
+            _lib.call("vs_conv1d_plan_create", _algo(algorithm), int(correlate), self.x_len,
+                      ptr(hr), self.h_len, self.h_len, self.n_filters,
+                      ctypes.byref(self._plan), stream_of(h))
+        algo, pre = ctypes.c_int(), ctypes.c_int()
+        _lib.call("vs_conv1d_plan_info", self._plan, ctypes.byref(algo), ctypes.byref(pre))
+        self.algorithm = {v: k for k, v in ALGORITHMS.items()}.get(algo.value, algo.value)
+        self.precomputed = bool(pre.value)
+        self._stream_used = torch.cuda.current_stream(h.device)
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        if x.shape[-1] != self.x_len or x.dtype != torch.float32 or x.device != self.device:
+            raise ValueError("Conv1dPlan: x must be float32 [..., x_len] on the plan's device")
+        xr, lead = _rows(x)
+        batch = xr.shape[0]
+        ylen = self.x_len + self.h_len - 1
+        y = torch.empty((batch, ylen), dtype=torch.float32, device=x.device)
+        self._stream_used = torch.cuda.current_stream(x.device)
+        with on_device(x):
+            _lib.call("vs_conv1d_plan_execute", self._plan, ptr(xr), self.x_len, ptr(y), ylen,
+                      batch, stream_of(x))
+        return y.reshape(*lead, ylen)
+
+    def __del__(self):
+        plan = getattr(self, "_plan", None)
+        if plan is not None and plan.value:
+            try:
+                self._stream_used.synchronize()   # executions queued on it still read the plan
+                _lib.lib().vs_conv1d_plan_destroy(plan)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+            self._plan = ctypes.c_void_p()
 
 
 def _conv_setup(ctx, inputs, output):
