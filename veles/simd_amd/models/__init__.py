@@ -14,6 +14,23 @@ from torch import nn
 from .. import ops
 
 
+def _cached_plan(mod: nn.Module, taps: torch.Tensor, x: torch.Tensor, algorithm,
+                 correlate: bool):
+    """Inference with fixed taps on the GPU: a Conv1dPlan (filter spectra
+    computed once) cached on `mod`, keyed by signal length, device and the
+    taps' storage and version counter; None when autograd or the CPU path
+    applies."""
+    if (not x.is_cuda or x.dtype != torch.float32 or taps.requires_grad
+            and torch.is_grad_enabled()):
+        return None
+    key = (x.shape[-1], x.device, taps._version, taps.data_ptr(), correlate)
+    if getattr(mod, "_plan_key", None) != key:
+        mod._plan = ops.Conv1dPlan(taps.detach().to(x.device), x.shape[-1], algorithm,
+                                   correlate=correlate)
+        mod._plan_key = key
+    return mod._plan
+
+
 class FIRFilter(nn.Module):
     """y = x (*) h along the last dim.  mode: "full" (x+h-1 samples, the
     reference convolve.h contract), "same" (len x, centred) or "valid".
@@ -33,18 +50,7 @@ class FIRFilter(nn.Module):
         self.algorithm = algorithm
 
     def _planned(self, x: torch.Tensor):
-        """Inference with fixed taps on the GPU: a cached Conv1dPlan (filter
-        spectra computed once) keyed by signal length, device and the taps'
-        version counter; None when autograd or the CPU path applies."""
-        if (not x.is_cuda or x.dtype != torch.float32 or self.taps.requires_grad
-                and torch.is_grad_enabled()):
-            return None
-        key = (x.shape[-1], x.device, self.taps._version, self.taps.data_ptr())
-        if getattr(self, "_plan_key", None) != key:
-            self._plan = ops.Conv1dPlan(self.taps.detach().to(x.device), x.shape[-1],
-                                        self.algorithm)
-            self._plan_key = key
-        return self._plan
+        return _cached_plan(self, self.taps, x, self.algorithm, False)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         plan = self._planned(x)
@@ -69,7 +75,8 @@ class MatchedFilter(nn.Module):
         self.threshold = threshold
 
     def forward(self, x: torch.Tensor):
-        resp = ops.correlate(x, self.template)
+        plan = _cached_plan(self, self.template, x, "auto", True)
+        resp = plan(x) if plan is not None else ops.correlate(x, self.template)
         out = []
         for row in resp.reshape(-1, resp.shape[-1]):
             pos, val = ops.detect_peaks(row, ops.signal.MAXIMUM)
