@@ -35,7 +35,7 @@
 
 namespace vs {
 namespace conv {
-extern int g_conv_buf, g_conv_real, g_conv_real_all;  // tuning knobs, defined below
+extern int g_conv_buf, g_conv_real, g_conv_real_all, g_conv_fused4;  // tuning knobs, defined below
 namespace {
 
 using fft::cmul;
@@ -846,6 +846,9 @@ int g_os_log_max = fft::kMaxLdsLog + 1;
 //   h = 700: 344 -> 388 K, 1000: 260 -> 336 K, 2000: 270 -> 330 K;
 //   h = 3000 / 4096 keep L = 8192 / 16384 (L = 16384 / 32768: -7 % / -14 %).
 int g_os_extra = 0;
+// Tuning knob (vs_tune_set("conv_fused4", 0/1)): fused three-pass four-step
+// FFT convolution (fft::conv_four_step) vs the seven-pass sequence.
+int g_conv_fused4 = 1;
 // Tuning knob (vs_tune_set("conv_buffer", 0/1)): buffer-descriptor loads and
 // stores in the fused block kernels.
 int g_conv_buf = 1;
@@ -886,13 +889,13 @@ int select(int xlen, int hlen, int batch) {
   // (405 vs 267 Gsamples/s, profiles/r1/conv_sweep_v2.log).
   if (ylen <= 64 || hlen <= 8 || (hlen <= 32 && xlen < 4096)) return VS_CONV_DIRECT;
   const int los = os_block_log(hlen);
-  // Overlap-save while >= 15 % of each block is useful output: the block rule
-  // keeps >= 75 % up to h = 8192; past that L = 32768 real blocks still beat
-  // the whole-signal four-step FFT (~45 Gsamples/s at 2^20 x 64) down to
-  // ~12 % useful -- h = 20000 (39 %): 144 vs 45; h = 30000 (8 %): 36 vs 45
-  // (profiles/r2/conv/conv_long.log).
+  // Overlap-save while >= 20 % of each block is useful output: the block rule
+  // keeps >= 75 % up to h = 8192; past that L = 32768 real blocks (~370 M block
+  // points/s at 2^20 x 64) still beat the whole-signal four-step FFT (fused,
+  // ~73 Gsamples/s) down to ~20 % useful -- h = 20000 (39 %): 144 vs 73
+  // (profiles/r2/conv/conv_long.log, f4_ab.log).
   const bool os_ok = static_cast<long long>((1 << los) - (hlen - 1)) * 100 >=
-                     15LL * (1 << los);
+                     20LL * (1 << los);
   int lm = 1;
   while ((1LL << lm) < ylen) lm++;
   if (lm <= max_block_log() && (!os_ok || ylen <= (1LL << los)))
@@ -1107,6 +1110,10 @@ vs_status run_fft_large(int correlate, const float *x, int xlen, int64_t xs,
                      s, h, hlen, hs, correlate, logm, 1, hz.as<float2>());
   VS_TRY(fft::launch_cols(logm, false, hz.as<float2>(), hz.as<float2>(), 1, s));
   VS_TRY(fft::launch_c2c_lds(log2, false, hz.as<float2>(), hz.as<float2>(), 1 << log1, s));
+  if (g_conv_fused4) {
+    return fft::conv_four_step(logm, x, xlen, xs, batch, hz.as<float2>(), y, ys, ylen,
+                               z.as<float2>(), s);
+  }
   hipLaunchKernelGGL(pack_pairs_kernel, dim3(elementwise_grid(M * npairs, 256)),
                      dim3(256), 0, s, x, xlen, xs, batch, logm, npairs, z.as<float2>());
   VS_TRY(fft::launch_cols(logm, false, z.as<float2>(), z.as<float2>(), npairs, s));
@@ -1371,6 +1378,10 @@ vs_status vs_tune_set(const char *key, int value) {
   if (std::strcmp(key, "conv_real") == 0) {
     VS_REQUIRE(value >= 0 && value <= 2, "conv_real must be 0, 1 or 2");
     conv::g_conv_real = value;
+    return VS_OK;
+  }
+  if (std::strcmp(key, "conv_fused4") == 0) {
+    conv::g_conv_fused4 = value < 0 ? 1 : value != 0;
     return VS_OK;
   }
   if (std::strcmp(key, "conv_real_all") == 0) {

@@ -294,6 +294,155 @@ void launch_cols_t(bool inv, const float2 *in, float2 *out, int log2n2,
                        in, out, log2n2, tw1, tws, sh);
 }
 
+
+// ----------------------------------------- fused four-step FFT convolution
+// conv_four_step: the whole-signal FFT convolution (filters longer than an
+// overlap-save block) in three passes over the data instead of seven:
+//   cols_pack_kernel   real signal pairs (2p, 2p+1) -> z, forward column FFT
+//                      with twiddles (replaces pack + cols);
+//   rows_conv_kernel   row FFT -> x H (same permuted layout) -> inverse row
+//                      FFT with reversed radices, in registers / LDS
+//                      (replaces rows + multiply + inverse rows);
+//   cols_unpack_kernel inverse column FFT -> scaled outputs of both signals
+//                      straight to y (replaces inverse cols + unpack).
+template <int LOG1>
+__global__ __launch_bounds__(ColGeom<LOG1>::kThreads) void cols_pack_kernel(
+    const float *__restrict__ x, int xlen, int64_t xs, int batch, float2 *__restrict__ out,
+    int log2n2, const float2 *__restrict__ tw1, const float2 *__restrict__ tws, int s) {
+  using PL = Plan<LOG1>;
+  constexpr int COLS = ColGeom<LOG1>::COLS;
+  __shared__ float2 lds[COLS * PL::kLds];
+  const long long n2 = 1LL << log2n2;
+  const long long N = n2 << LOG1;
+  const int cl = threadIdx.x % COLS, t = threadIdx.x / COLS;
+  const long long col = static_cast<long long>(blockIdx.x) * COLS + cl;
+  const long long s0 = 2LL * blockIdx.y, s1 = s0 + 1;
+  const float *x0 = x + s0 * xs;
+  const float *x1 = x + (s1 < batch ? s1 : s0) * xs;
+  const bool has1 = s1 < batch;
+  float2 *dst = out + blockIdx.y * N + col;
+  float2 v[PL::E];
+  constexpr int R0 = PL::first_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+    for (int j = 0; j < R0; j++) {
+      const long long n = static_cast<long long>(reg_index<PL, R0>(t, b, j)) * n2 + col;
+      const bool in = n < xlen;
+      v[b * R0 + j] = make_float2(in ? x0[n] : 0.f, in && has1 ? x1[n] : 0.f);
+    }
+  transform<PL, false, false>(v, lds + cl * PL::kLds, t, tw1);
+  constexpr int RL = PL::last_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+      const int k1 = reg_index<PL, RL>(t, b, j);
+      dst[static_cast<long long>(k1) * n2] = cmul(v[b * RL + j], split_root(tws, s, col * k1));
+    }
+}
+
+// One row (n2 = 2^LOG2 points, contiguous) per workgroup: forward FFT,
+// times H of the same row, inverse FFT with the radices reversed so the
+// spectrum never leaves the registers between the two transforms.
+template <int LOG2>
+__global__ __launch_bounds__(Plan<LOG2>::TPS) void rows_conv_kernel(
+    float2 *__restrict__ z, const float2 *__restrict__ H, int log1, const float2 *__restrict__ tw) {
+  using PL = Plan<LOG2>;
+  __shared__ float2 lds[PL::kLds];
+  const int t = threadIdx.x;
+  const long long rows = 1LL << log1;
+  const long long row = blockIdx.x;                  // row within the pair's matrix
+  float2 *zr = z + (static_cast<long long>(blockIdx.y) * rows + row) * PL::N;
+  const float2 *hr = H + row * PL::N;
+  float2 v[PL::E];
+  constexpr int R0 = PL::first_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+    for (int j = 0; j < R0; j++) v[b * R0 + j] = zr[reg_index<PL, R0>(t, b, j)];
+  __builtin_amdgcn_sched_barrier(0);
+  transform<PL, false, false>(v, lds, t, tw);
+  constexpr int RL = PL::last_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++)
+      v[b * RL + j] = cmul(v[b * RL + j], hr[reg_index<PL, RL>(t, b, j)]);
+  transform<PL, true, true>(v, lds, t, tw);
+  constexpr int RI = PL::radix(0);
+#pragma unroll
+  for (int b = 0; b < PL::E / RI; b++)
+#pragma unroll
+    for (int j = 0; j < RI; j++) zr[reg_index<PL, RI>(t, b, j)] = v[b * RI + j];
+}
+
+template <int LOG1>
+__global__ __launch_bounds__(ColGeom<LOG1>::kThreads) void cols_unpack_kernel(
+    const float2 *__restrict__ in, int log2n2, int batch, float *__restrict__ y, int64_t ys,
+    int ylen, float scale, const float2 *__restrict__ tw1, const float2 *__restrict__ tws,
+    int s) {
+  using PL = Plan<LOG1>;
+  constexpr int COLS = ColGeom<LOG1>::COLS;
+  __shared__ float2 lds[COLS * PL::kLds];
+  const long long n2 = 1LL << log2n2;
+  const long long N = n2 << LOG1;
+  const int cl = threadIdx.x % COLS, t = threadIdx.x / COLS;
+  const long long col = static_cast<long long>(blockIdx.x) * COLS + cl;
+  const float2 *src = in + blockIdx.y * N + col;
+  const long long s0 = 2LL * blockIdx.y, s1 = s0 + 1;
+  float *y0 = y + s0 * ys;
+  float *y1 = y + s1 * ys;
+  const bool has1 = s1 < batch;
+  float2 v[PL::E];
+  constexpr int R0 = PL::first_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / R0; b++)
+#pragma unroll
+    for (int j = 0; j < R0; j++) {
+      const int k1 = reg_index<PL, R0>(t, b, j);
+      v[b * R0 + j] = cmulc(src[static_cast<long long>(k1) * n2], split_root(tws, s, col * k1));
+    }
+  transform<PL, true, false>(v, lds + cl * PL::kLds, t, tw1);
+  constexpr int RL = PL::last_radix(false);
+#pragma unroll
+  for (int b = 0; b < PL::E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+      const long long n = static_cast<long long>(reg_index<PL, RL>(t, b, j)) * n2 + col;
+      if (n < ylen) {
+        y0[n] = v[b * RL + j].x * scale;
+        if (has1) y1[n] = v[b * RL + j].y * scale;
+      }
+    }
+}
+
+template <int LOG1>
+void launch_pack_t(const float *x, int xlen, int64_t xs, int batch, float2 *z, int log2n2,
+                   const float2 *tw1, const float2 *tws, int sh, hipStream_t s) {
+  using G = ColGeom<LOG1>;
+  const dim3 grid(static_cast<unsigned>((1LL << log2n2) / G::COLS),
+                  static_cast<unsigned>((batch + 1) / 2));
+  hipLaunchKernelGGL((cols_pack_kernel<LOG1>), grid, dim3(G::kThreads), 0, s, x, xlen, xs,
+                     batch, z, log2n2, tw1, tws, sh);
+}
+
+template <int LOG1>
+void launch_unpack_t(const float2 *z, int log2n2, int batch, float *y, int64_t ys, int ylen,
+                     float scale, const float2 *tw1, const float2 *tws, int sh, hipStream_t s) {
+  using G = ColGeom<LOG1>;
+  const dim3 grid(static_cast<unsigned>((1LL << log2n2) / G::COLS),
+                  static_cast<unsigned>((batch + 1) / 2));
+  hipLaunchKernelGGL((cols_unpack_kernel<LOG1>), grid, dim3(G::kThreads), 0, s, z, log2n2,
+                     batch, y, ys, ylen, scale, tw1, tws, sh);
+}
+
+template <int LOG2>
+void launch_rows_conv_t(float2 *z, const float2 *H, int log1, int npairs, const float2 *tw,
+                        hipStream_t s) {
+  hipLaunchKernelGGL((rows_conv_kernel<LOG2>), dim3(1u << log1, static_cast<unsigned>(npairs)),
+                     dim3(Plan<LOG2>::TPS), 0, s, z, H, log1, tw);
+}
 }  // namespace
 
 vs_status launch_c2c_lds(int logn, bool inv, const float2 *in, float2 *out,
@@ -366,6 +515,49 @@ vs_status c2c(int logn, bool inv, const float2 *in, float2 *out, int batch,
   VS_TRY(launch_transpose(log2, log1, in, t, batch, s));
   VS_TRY(launch_c2c_lds(log2, true, t, t, batch << log1, s));
   return launch_cols(logn, true, t, out, batch, s);
+}
+
+
+vs_status conv_four_step(int logm, const float *x, int xlen, int64_t xs, int batch,
+                         const float2 *H, float *y, int64_t ys, int ylen, float2 *z,
+                         hipStream_t s) {
+  int log1, log2;
+  four_step_split(logm, &log1, &log2);
+  VS_REQUIRE(log1 >= 1 && log1 <= 10 && log2 >= 5 && log2 <= kMaxLdsLog,
+             "four-step convolution: bad split of 2^%d", logm);
+  vs_status st;
+  const float2 *tw1 = twiddles(log1, &st);
+  if (!tw1) return st;
+  const float2 *tw2 = twiddles(log2, &st);
+  if (!tw2) return st;
+  const float2 *tws = split_twiddles(logm, &st);
+  if (!tws) return st;
+  const int sh = split_shift(logm);
+  const int npairs = (batch + 1) / 2;
+  switch (log1) {
+#define VS_CASE(L) \
+  case L: launch_pack_t<L>(x, xlen, xs, batch, z, log2, tw1, tws, sh, s); break;
+    VS_CASE(1) VS_CASE(2) VS_CASE(3) VS_CASE(4) VS_CASE(5) VS_CASE(6) VS_CASE(7)
+    VS_CASE(8) VS_CASE(9) VS_CASE(10)
+#undef VS_CASE
+  }
+  switch (log2) {
+#define VS_CASE(L) \
+  case L: launch_rows_conv_t<L>(z, H, log1, npairs, tw2, s); break;
+    VS_CASE(5) VS_CASE(6) VS_CASE(7) VS_CASE(8) VS_CASE(9) VS_CASE(10) VS_CASE(11)
+    VS_CASE(12) VS_CASE(13) VS_CASE(14)
+#undef VS_CASE
+  }
+  const float scale = 1.0f / static_cast<float>(1LL << logm);
+  switch (log1) {
+#define VS_CASE(L) \
+  case L: launch_unpack_t<L>(z, log2, batch, y, ys, ylen, scale, tw1, tws, sh, s); break;
+    VS_CASE(1) VS_CASE(2) VS_CASE(3) VS_CASE(4) VS_CASE(5) VS_CASE(6) VS_CASE(7)
+    VS_CASE(8) VS_CASE(9) VS_CASE(10)
+#undef VS_CASE
+  }
+  VS_HIP(hipGetLastError());
+  return VS_OK;
 }
 
 }  // namespace fft

@@ -42,6 +42,13 @@ vs_status launch_c2c_lds(int logn, bool inverse, const float2 *in, float2 *out,
 // inverse: * conj W_N^(n2 k1), then IFFT_N1 over columns.
 vs_status launch_cols(int logn, bool inverse, const float2 *in, float2 *out,
                       int batch, hipStream_t s);
+// Whole-signal FFT convolution of `batch` real signals (packed in pairs into
+// z: (batch + 1) / 2 x 2^logm complex scratch) with the four-step-layout
+// filter spectrum H (cols + rows forward of the padded filter): three fused
+// passes, outputs scaled by 2^-logm straight to y (ylen per row).
+vs_status conv_four_step(int logm, const float *x, int xlen, int64_t xs, int batch,
+                         const float2 *H, float *y, int64_t ys, int ylen, float2 *z,
+                         hipStream_t s);
 // out[sig][k1 + N1 k2] = in[sig][k1][k2]  (N1 x N2 -> natural order).
 vs_status launch_transpose(int log1, int log2, const float2 *in, float2 *out,
                            int batch, hipStream_t s);

@@ -191,8 +191,8 @@ def test_partitioned_beyond_32768_block():
 
 
 def test_select_long_filter_overlap_save():
-    """Filters whose L = 32768 block is >= 15 % useful run overlap-save
-    (h = 20000: 144 vs 45 Gsamples/s for the four-step FFT); shorter blocks
+    """Filters whose L = 32768 block is >= 20 % useful run overlap-save
+    (h = 20000: 144 vs 73 Gsamples/s for the fused four-step FFT); shorter blocks
     fall back to the FFT (profiles/r2/conv/conv_long.log)."""
     from veles.simd_amd import _lib
     lib = _lib.lib()
@@ -200,3 +200,24 @@ def test_select_long_filter_overlap_save():
     assert lib.vs_conv1d_select(1 << 20, 30000, 64) == 2
     _check(200000, 20000, 2, "auto", False)
     _check(200000, 20000, 1, "auto", True)
+
+
+@pytest.mark.parametrize("xlen,hlen,batch", [(300000, 40000, 3), (100003, 60000, 2),
+                                             (40000, 30000, 1)])
+@pytest.mark.parametrize("corr", [False, True])
+def test_fused_four_step_conv(xlen, hlen, batch, corr):
+    """Whole-signal FFT convolution through the fused three-pass four-step
+    kernels (fft.hip conv_four_step: pack + columns, rows x H x inverse rows,
+    inverse columns + unpack) against fp64, and equal to the seven-pass
+    sequence (vs_tune_set conv_fused4 = 0) up to rounding."""
+    import torch
+    from veles.simd_amd import ops
+    _check(xlen, hlen, batch, "fft", corr)
+    g = torch.Generator().manual_seed(xlen)
+    x = torch.randn(batch, xlen, generator=g).cuda()
+    h = torch.randn(hlen, generator=g).cuda()
+    y1 = ops.conv1d(x, h, algorithm="fft", correlate=corr)
+    with _knob("conv_fused4", 0, 1):
+        y0 = ops.conv1d(x, h, algorithm="fft", correlate=corr)
+    scale = y0.abs().max().item()
+    assert (y1 - y0).abs().max().item() <= 1e-5 * scale
