@@ -116,8 +116,8 @@ def test_four_step_fft_conv_2p23():
     """x + h - 1 just above 2^22 -> a 2^23-point four-step transform."""
     from veles.simd_amd import _lib
     xlen, hlen = (1 << 22) + 4096 - 20000 + 1, 20000
-    # auto picks overlap-save here (L = 32768 blocks, 39 % useful, since the
-    # 15 % rule); the explicit FFT request below still runs the 2^23 transform
+    # auto picks overlap-save here (L = 32768 blocks, 39 % useful, under the
+    # 20 % rule); the explicit FFT request below still runs the 2^23 transform
     assert _lib.lib().vs_conv1d_select(xlen, hlen, 1) == 3
     _check(xlen, hlen, 1, "fft", False)
     _check(xlen, hlen, 1, "fft", True)
