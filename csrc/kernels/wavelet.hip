@@ -553,6 +553,11 @@ vs_status launch_swt_tiled(const Taps &t, int ext, int levels, const float *src,
 // hi stores (+3 % on db8 x 8 levels: the hi rows are never re-read here).
 int g_swt_fused = 1;
 int g_swt_nt = 1;
+// "dwt_vec" 1 (default) = vectorised pyramid kernel (dwt_multi4_kernel),
+// 0 = the scalar round-1 kernel.
+int g_dwt_vec = 1;
+// "dwt_threads": workgroup size of the vectorised pyramid (0 = auto).
+int g_dwt_threads = 0;
 
 template <int ORDER>
 vs_status launch_swt_multi4(const Taps &t, int ext, int levels, const float *src, int len,
@@ -659,6 +664,108 @@ __global__ __launch_bounds__(256) void dwt_multi_t_kernel(
   for (int k = threadIdx.x; k < n; k += blockDim.x) orow[off + k] = in[k];
 }
 
+// Vectorised pyramid (round 2): float4 input loads, four consecutive outputs
+// per lane from a float4 register window (inputs 2k .. 2k + 6 + ORDER - 1),
+// float4 hi stores and low-band writes; the two LDS bands are len and len / 2
+// (+ pads) so three 8192-sample workgroups share a CU.  Levels whose half
+// length is not a multiple of 4 run the scalar loop.  Measured (65536 x 1024
+// / 8192 x 8192, db8, 5 levels): profiles/r2/swt/dwt.md.
+template <int ORDER>
+__global__ __launch_bounds__(256) void dwt_multi4_kernel(
+    Taps taps, int ext, int levels, const float *__restrict__ src, int len,
+    float *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float dband4[];
+  constexpr int kPad = 16 + ORDER;
+  float hp[ORDER], lp[ORDER];
+#pragma unroll
+  for (int r = 0; r < ORDER; r++) {
+    hp[r] = taps.hp[r];
+    lp[r] = taps.lp[r];
+  }
+  const int64_t sig = blockIdx.x;
+  const float *x = src + sig * len;
+  float *orow = out + sig * len;
+  float *bandA = dband4, *bandB = dband4 + ((len + kPad + 3) & ~3);
+  for (int q = threadIdx.x; q < len / 4; q += blockDim.x)
+    reinterpret_cast<float4 *>(bandA)[q] = reinterpret_cast<const float4 *>(x)[q];
+  __syncthreads();  // the level-0 extension reads samples other lanes loaded
+  float *in = bandA, *nxt = bandB;
+  int n = len, off = 0;
+  for (int l = 0; l < levels; l++) {
+    const int half = n / 2;
+    for (int t = threadIdx.x; t < ORDER; t += blockDim.x) {
+      const int j = ext_index(n + t, n, ext);
+      in[n + t] = j < 0 ? 0.f : in[j];
+    }
+    __syncthreads();
+    if (half % 4 == 0) {
+      constexpr int W = (6 + ORDER + 3) / 4;  // float4 window per 4 outputs
+      for (int q = threadIdx.x; q < half / 4; q += blockDim.x) {
+        float w[4 * W];
+#pragma unroll
+        for (int c = 0; c < W; c++) {
+          const float4 v = reinterpret_cast<const float4 *>(in + 8 * q)[c];
+          w[4 * c] = v.x;
+          w[4 * c + 1] = v.y;
+          w[4 * c + 2] = v.z;
+          w[4 * c + 3] = v.w;
+        }
+        float sh[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < ORDER; j++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            sh[e] = fmaf(hp[j], w[2 * e + j], sh[e]);
+            sl[e] = fmaf(lp[j], w[2 * e + j], sl[e]);
+          }
+        reinterpret_cast<float4 *>(orow + off)[q] = make_float4(sh[0], sh[1], sh[2], sh[3]);
+        reinterpret_cast<float4 *>(nxt)[q] = make_float4(sl[0], sl[1], sl[2], sl[3]);
+      }
+    } else {
+      for (int k = threadIdx.x; k < half; k += blockDim.x) {
+        float sh = 0.f, sl = 0.f;
+#pragma unroll
+        for (int j = 0; j < ORDER; j++) {
+          const float v = in[2 * k + j];
+          sh = fmaf(hp[j], v, sh);
+          sl = fmaf(lp[j], v, sl);
+        }
+        orow[off + k] = sh;
+        nxt[k] = sl;
+      }
+    }
+    __syncthreads();
+    float *t = in;  // the new low band becomes the input
+    in = nxt;
+    nxt = t;
+    off += half;
+    n = half;
+  }
+  for (int k = threadIdx.x; k < n; k += blockDim.x) orow[off + k] = in[k];
+}
+
+template <int ORDER>
+vs_status launch_dwt_multi4(const Taps &t, int ext, int levels, const float *src, int len,
+                            float *out, int batch, hipStream_t s) {
+  constexpr int kPad = 16 + ORDER;
+  const size_t lds = (((len + kPad + 3) & ~3) + len / 2 + kPad) * sizeof(float);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(dwt_multi4_kernel<ORDER>),
+      hipFuncAttributeMaxDynamicSharedMemorySize,
+      (((kDwtMultiMax + kPad + 3) & ~3) + kDwtMultiMax / 2 + kPad) * 4);
+  VS_HIP(attr);
+  // About 16 samples per lane (two quads at level 0): 1024-sample signals
+  // run 64-lane workgroups (+31 % db2, +48 % db8 over 256 lanes), 8192 and
+  // longer 256 (profiles/r2/swt/dwt.md).
+  int threads = std::min(256, std::max(64, (len / 16 + 63) / 64 * 64));
+  if (g_dwt_threads >= 64 && g_dwt_threads <= 256 && g_dwt_threads % 64 == 0)
+    threads = g_dwt_threads;
+  hipLaunchKernelGGL(dwt_multi4_kernel<ORDER>, dim3(static_cast<unsigned>(batch)), dim3(threads),
+                     lds, s, t, ext, levels, src, len, out);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
 template <int ORDER>
 vs_status launch_dwt_multi_t(const Taps &t, int ext, int levels, const float *src, int len,
                              float *out, int batch, hipStream_t s) {
@@ -711,6 +818,14 @@ bool tune(const char *key, int value) {
   }
   if (std::strcmp(key, "swt_nt") == 0) {
     g_swt_nt = value < 0 ? 1 : value;
+    return true;
+  }
+  if (std::strcmp(key, "dwt_vec") == 0) {
+    g_dwt_vec = value < 0 ? 1 : value;
+    return true;
+  }
+  if (std::strcmp(key, "dwt_threads") == 0) {
+    g_dwt_threads = value < 0 ? 0 : value;
     return true;
   }
   return false;
@@ -889,6 +1004,18 @@ vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,
     VS_HIP(hipMemcpy2DAsync(out + off, len * sizeof(float), in, n * sizeof(float),
                             n * sizeof(float), rows, hipMemcpyDeviceToDevice, s));
     return VS_OK;
+  }
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(out)) &
+                        15) == 0;
+  if (g_dwt_vec && len % 4 == 0 && aligned) {
+    switch (order) {
+#define VS_DWT_V(O) \
+  case O: return launch_dwt_multi4<O>(t, ext, levels, src, len, out, batch, s);
+      VS_DWT_V(2) VS_DWT_V(4) VS_DWT_V(6) VS_DWT_V(8) VS_DWT_V(12) VS_DWT_V(16) VS_DWT_V(18)
+      VS_DWT_V(20) VS_DWT_V(24) VS_DWT_V(30)
+#undef VS_DWT_V
+      default: break;
+    }
   }
   switch (order) {
 #define VS_DWT_T(O) \

@@ -303,3 +303,49 @@ def test_swt_multilevel_long_tiled(t, o, levels, n, e):
                                        err_msg=f"level {lvl}")
             cur[r] = vlo
     np.testing.assert_allclose(lo.numpy(), cur, atol=3e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,o,levels,n", [(D, 8, 5, 8192), (D, 2, 10, 1024), (C, 30, 4, 512),
+                                          (S, 16, 3, 24), (D, 4, 4, 16384), (D, 6, 2, 100)])
+@pytest.mark.parametrize("e", EXTS)
+def test_dwt_multilevel_vec(t, o, levels, n, e):
+    """LDS pyramid (vs_dwt_multilevel): vectorised kernel (dwt_multi4_kernel;
+    (S, 16, 3, 24) and (D, 6, 2, 100) have levels whose half length is not a
+    multiple of 4 and take its scalar loop) against the scalar kernel
+    (vs_tune_set dwt_vec 0) and the level-by-level host reference."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(o + levels + e + n)
+    b = 3
+    x = torch.randn(b, n, generator=g)
+    xd = x.cuda()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for vec in (1, 0):
+        out = torch.full((b, n), float("nan"), device="cuda")
+        assert lib.vs_tune_set(b"dwt_vec", vec) == 0
+        try:
+            st = lib.vs_dwt_multilevel(t, o, levels, e, ctypes.c_void_p(xd.data_ptr()), n,
+                                       ctypes.c_void_p(out.data_ptr()), b, s)
+            assert st == 0, lib.vs_last_error()
+            torch.cuda.synchronize()
+        finally:
+            lib.vs_tune_set(b"dwt_vec", -1)
+        outs.append(out.cpu())
+    torch.testing.assert_close(outs[0], outs[1], atol=1e-5, rtol=0)
+    pyr = outs[0].numpy()
+    cur = x.numpy()
+    off = 0
+    for lvl in range(levels):
+        m = cur.shape[1] // 2
+        nxt = np.zeros((b, m), np.float32)
+        for r in range(b):
+            vhi, vlo = capi.wavelet_apply(t, o, e, cur[r], na=True)
+            np.testing.assert_allclose(pyr[r, off:off + m], vhi, atol=5e-4, err_msg=f"level {lvl}")
+            nxt[r] = vlo
+        cur = nxt
+        off += m
+    np.testing.assert_allclose(pyr[:, off:], cur, atol=5e-4)
