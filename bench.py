@@ -227,8 +227,8 @@ def main():
             if st:
                 raise RuntimeError(lib.vs_last_error().decode())
 
-        ssteps = max(5, args.steps // 2)
-        dts = _timed(swt_step, ssteps, 2, dist_on)
+        ssteps = max(20, args.steps)
+        dts = _timed(swt_step, ssteps, 5, dist_on)
         secondary.update({
             "swt_dp_msamples_per_s": round(total * sn * ssteps / dts / 1e6, 1),
             "swt_dp_ms_per_step": round(dts / ssteps * 1e3, 3),
