@@ -39,7 +39,7 @@ CONV_BATCH = 64
 
 def _baseline():
     """Reference numbers this run is divided by (None if none)."""
-    path = os.path.join(REPO, "profiles", "reference_cpu_baseline.json")
+    path = os.path.join(REPO, "bench", "reference_cpu_baseline.json")
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f)
@@ -52,7 +52,35 @@ def _sync_all(dist_on):
     torch.cuda.synchronize()
 
 
+# The GPU ramps its clock over the first ~25 ms of sustained load: measured
+# per-call SGEMM 4096^3 from a cold start (tools/probes/warm_curve.py,
+# profiles/r2/session6/warm_curve.md) runs 105 TF over calls 0-5, 132 over
+# 5-10, 140 over 10-25 and a flat 143 from call 25 on.  A driver run of
+# --warmup 5 --steps 20 would time the ramp, not the kernel, so every timed
+# section first keeps the device busy for DEVICE_WARM_S of untimed calls of
+# the same step, THEN runs the W warmup steps and times exactly K steps.
+DEVICE_WARM_S = 0.25
+
+
+def _device_warm(fn, dist_on):
+    """Untimed calls of `fn` for ~DEVICE_WARM_S; every rank runs the same
+    count (max over ranks) so collectives inside `fn` stay matched."""
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    one = max(time.perf_counter() - t0, 1e-5)
+    count = min(2000, int(DEVICE_WARM_S / one))
+    if dist_on:
+        t = torch.tensor([count], dtype=torch.int64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        count = int(t.item())
+    for _ in range(count):
+        fn()
+    return count + 1
+
+
 def _timed(fn, steps, warmup, dist_on):
+    _device_warm(fn, dist_on)
     for _ in range(warmup):
         fn()
     _sync_all(dist_on)
@@ -267,6 +295,7 @@ def main():
             "config": {"model": "sgemm_4096x4096x4096_fp32",
                        "global_batch": world, "seq_len": n,
                        "parallelism": f"dp{world}"},
+            "device_warmup_s": DEVICE_WARM_S,
             "secondary": secondary,
         }), flush=True)
     if dist_on:

@@ -9,7 +9,7 @@ flags (-O2 -march=native, common.ac:267) into a scratch directory and times
     convolution; the FFT / overlap-save paths need the external FFTF library,
     which is not available offline -- a stub header satisfies the include,
     those paths are not timed: "parity unpinned").
-Results go to profiles/reference_cpu_baseline.json, which bench.py divides by.
+Results go to bench/reference_cpu_baseline.json, which bench.py divides by.
 Only runs where /root/reference exists (the build container).
 """
 import json
@@ -94,7 +94,7 @@ def main():
     res["source"] = ("reference src/matrix.c + src/convolve.c compiled -O2 -march=native, "
                      f"one core of: {cpu}")
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
-    with open(os.path.join(REPO, "profiles", "reference_cpu_baseline.json"), "w") as f:
+    with open(os.path.join(REPO, "bench", "reference_cpu_baseline.json"), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
     return 0
