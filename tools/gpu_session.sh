@@ -41,7 +41,7 @@ if [ "$MODE" = "tests" ] || [ "$MODE" = "all" ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = "bench" ] || [ "$MODE" = "all" ]; then
-  step bench 600 python bench.py --steps 30 --warmup 5
+  step bench 600 python bench.py --steps 20 --warmup 5
 fi
 if [ "$MODE" = "prof" ] || [ "$MODE" = "all" ]; then
   export TMPDIR=/tmp
