@@ -64,19 +64,24 @@ DEVICE_WARM_S = 0.25
 
 def _device_warm(fn, dist_on):
     """Untimed calls of `fn` for ~DEVICE_WARM_S; every rank runs the same
-    count (max over ranks) so collectives inside `fn` stay matched."""
-    t0 = time.perf_counter()
+    count (max over ranks) so collectives inside `fn` stay matched.  The
+    first call (one-time setup: plans, twiddle tables, allocator growth) is
+    not used to size the count."""
     fn()
     torch.cuda.synchronize()
-    one = max(time.perf_counter() - t0, 1e-5)
-    count = min(2000, int(DEVICE_WARM_S / one))
+    t0 = time.perf_counter()
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    one = max((time.perf_counter() - t0) / 3, 1e-5)
+    count = min(5000, int(DEVICE_WARM_S / one))
     if dist_on:
         t = torch.tensor([count], dtype=torch.int64, device="cuda")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         count = int(t.item())
     for _ in range(count):
         fn()
-    return count + 1
+    return count + 4
 
 
 def _timed(fn, steps, warmup, dist_on):
@@ -179,7 +184,7 @@ def main():
             if st:
                 raise RuntimeError(lib.vs_last_error().decode())
 
-        csteps = max(5, args.steps // 2)
+        csteps = max(50, args.steps)  # ~0.25 ms per call: time >= 12 ms
         dtc = _timed(conv_step, csteps, max(2, args.warmup // 2), dist_on)
         msamples = CONV_LEN * CONV_BATCH * csteps * world / dtc / 1e6
         # Same convolution through a vs_conv1d plan (filter spectra computed
