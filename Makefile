@@ -11,6 +11,7 @@ BUILD    ?= build
 LIBDIR   := veles/simd_amd/_native
 LIB      := $(LIBDIR)/libvelessimd.so
 OPT      ?= -O3
+LDEXTRA  ?=
 
 COMMON   := $(OPT) -std=c++17 -fPIC -I. -Iinclude -Wall -Wextra \
             -Wno-unused-parameter -Wno-unused-command-line-argument \
@@ -37,7 +38,7 @@ lib: $(LIB)
 $(LIB): $(HIP_OBJS) $(CPP_OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -Wl,-soname,libvelessimd.so \
-	    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib $(LDEXTRA)
 
 $(BUILD)/%.o: %.hip $(HEADERS)
 	@mkdir -p $(dir $@)
@@ -113,6 +114,29 @@ asan:
 	    -L$(ASAN_BUILD)/lib -lvelessimd -Wl,-rpath,'$$ORIGIN/../lib'
 
 .PHONY: asan
+
+# Host line coverage (gcov), the counterpart of the reference's
+# --enable-test-coverage (common.ac:229-236): host code of every source built
+# with --coverage, then the native C test and the CPU pytest suite run
+# against that library; per-file line coverage in build-cov/coverage.txt.
+#   make coverage            (no GPU needed: host-reference paths)
+COV_BUILD := build-cov
+COV_FLAGS := -O2 -g -Xarch_host --coverage
+coverage:
+	$(MAKE) BUILD=$(COV_BUILD) OPT="$(COV_FLAGS)" LDEXTRA=--coverage \
+	    LIBDIR=$(COV_BUILD)/lib LIB=$(COV_BUILD)/lib/libvelessimd.so lib
+	@mkdir -p $(COV_BUILD)/tests
+	$(HIPCC) -O2 -g -std=c++17 -Iinclude -Itests/native \
+	    tests/native/capi_test.cpp -o $(COV_BUILD)/tests/capi_test \
+	    -L$(COV_BUILD)/lib -lvelessimd -Wl,-rpath,'$$ORIGIN/../lib'
+	find $(COV_BUILD) -name '*.gcda' -delete
+	VELES_DISABLE_GPU=1 $(COV_BUILD)/tests/capi_test > $(COV_BUILD)/capi_test.log
+	VELES_SIMD_LIB=$(CURDIR)/$(COV_BUILD)/lib/libvelessimd.so VELES_DISABLE_GPU=1 \
+	    python -m pytest tests -m "not gpu" -q -p no:cacheprovider > $(COV_BUILD)/pytest.log
+	python tools/coverage_report.py $(COV_BUILD) > $(COV_BUILD)/coverage.txt
+	tail -n 30 $(COV_BUILD)/coverage.txt
+
+.PHONY: coverage
 
 # Diagnostic build: per-phase s_memtime stamps in the real-block conv kernel
 # (tools/conv_stamps.py).  Not the shipped library.

@@ -49,8 +49,10 @@ def test_profile_ranges_wrap_native_calls():
         "torch.cuda.is_available = lambda: True\n"
         "torch.cuda.nvtx.range_push = lambda n: seen.append(('push', n))\n"
         "torch.cuda.nvtx.range_pop = lambda: seen.append(('pop',))\n"
-        "L.call('vs_gpu_available')\n"
-        "assert seen == [('push', 'vs_gpu_available'), ('pop',)], seen\n"
+        # a call whose result is 0 with or without a GPU (vs_gpu_available
+        # returns 1 on a GPU box, which call() would read as a failed status)
+        "L.call('vs_is_device_pointer', None)\n"
+        "assert seen == [('push', 'vs_is_device_pointer'), ('pop',)], seen\n"
         "print('ok')\n")
     out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True,
                          text=True, env=dict(os.environ, VELES_PROFILE_RANGES="1"))
