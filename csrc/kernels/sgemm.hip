@@ -341,16 +341,22 @@ bool launch_cfg5(const GemmArgs &g, int ta, int tb, bool vec, int batch, hipStre
 // base (A + m0 lda, ...), so offsets stay below 2^31 for any matrix whose
 // tile-row span fits (checked on the host).
 template <int BM_, int BN_, int WM_, int WN_, bool TA_, bool TB_, int DMA_, bool AGPR_,
-          int LDS_KB_ = 0>
+          int LDS_KB_ = 0, int G_ = 1>
 struct Cfg6 {
   static constexpr int BM = BM_, BN = BN_, BK = 16, WM = WM_, WN = WN_;
+  // barrier cadence: G = 1, a three-stage ring and a barrier every k tile;
+  // G = 2, 4, a ring of 2G stages and a barrier every G tiles (the DMAs of
+  // the next G tiles issued behind it)
+  static constexpr int G = G_, STAGES = G_ == 1 ? 3 : 2 * G_;
+  static_assert(G == 1 || G == 2 || G == 4, "barrier cadence");
   static constexpr bool TA = TA_, TB = TB_, AGPR = AGPR_;
   static constexpr bool AROWS = !TA, BROWS = TB;  // k-rows images
   static constexpr int DMA = DMA_;
   static constexpr int kThreads = 64 * WM * WN, kWaves = WM * WN;
   static constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   static constexpr int kImgA = BM * 64, kImgB = BN * 64, kStage = kImgA + kImgB;
-  static constexpr int kLdsBytes = 3 * kStage > LDS_KB_ * 1024 ? 3 * kStage : LDS_KB_ * 1024;
+  static constexpr int kLdsBytes =
+      STAGES * kStage > LDS_KB_ * 1024 ? STAGES * kStage : LDS_KB_ * 1024;
   static constexpr int kInstrBytes = 64 * DMA;  // bytes one wave instruction moves
   static constexpr int kInstrA = kImgA / kInstrBytes / kWaves;
   static constexpr int kInstrB = kImgB / kInstrBytes / kWaves;
@@ -358,7 +364,7 @@ struct Cfg6 {
   static_assert(kInstrA * kInstrBytes * kWaves == kImgA &&
                     kInstrB * kInstrBytes * kWaves == kImgB,
                 "tile not divisible into whole DMA instructions per wave");
-  static_assert(2 * kInstr < 64, "vmcnt immediates");
+  static_assert((STAGES - 1) * kInstr < 64, "vmcnt immediates");
   static constexpr int kReadsA = AROWS ? TM : 4 * TM, kReadsB = BROWS ? TN : 4 * TN;
 };
 
@@ -580,20 +586,20 @@ __global__ __launch_bounds__(C::kThreads) void sgemm6_kernel(GemmArgs g) {
   asm volatile("s_nop 7" ::: "memory");  // VALU write -> MFMA srcC read
 
   const int nk = (kn + C::BK - 1) / C::BK;
-  dma(0, 0);
-  if (nk > 1) dma(1, 1);
-  if (nk > 2) dma(2, 2);
-  if (nk > 2) wait_vmcnt<2 * C::kInstr>();
-  else if (nk > 1) wait_vmcnt<C::kInstr>();
-  else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem6));
   const auto off = K::offsets(arow, bcol, q);
   typename K::Frag f0, f1;
-  K::read_all(f0, K::at(lds0, off));
+  if constexpr (C::G == 1) {
+    dma(0, 0);
+    if (nk > 1) dma(1, 1);
+    if (nk > 2) dma(2, 2);
+    if (nk > 2) wait_vmcnt<2 * C::kInstr>();
+    else if (nk > 1) wait_vmcnt<C::kInstr>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    K::read_all(f0, K::at(lds0, off));
 
-  // tile kt: stage kt % 3, registers f[kt & 1] (see sgemm5_kernel)
+    // tile kt: stage kt % 3, registers f[kt & 1] (see sgemm5_kernel)
 #define VS_GEN6_STEP(CUR, NXT)                                                  \
   {                                                                             \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                          \
@@ -607,10 +613,46 @@ __global__ __launch_bounds__(C::kThreads) void sgemm6_kernel(GemmArgs g) {
     K::template mfma_half<2, true>(acc, CUR, NXT, K::at(sbase, off));           \
     kt++;                                                                       \
   }
-  int sc = 0;
-  for (int kt = 0; kt < nk;) {
-    VS_GEN6_STEP(f0, f1)
-    if (kt < nk) VS_GEN6_STEP(f1, f0)
+    int sc = 0;
+    for (int kt = 0; kt < nk;) {
+      VS_GEN6_STEP(f0, f1)
+      if (kt < nk) VS_GEN6_STEP(f1, f0)
+    }
+  } else {
+    // ring of S = 2G stages, stage of tile kt = kt % S.  Prologue: tiles
+    // 0..G.  At tiles kt = 0 mod G: wait for this wave's DMAs (tiles
+    // kt+1..kt+G, issued one barrier ago), barrier, then refill the stages
+    // of tiles kt-G+1..kt -- every wave has read them (tile kt's reads were
+    // waited at its start) -- with tiles kt+G+1..kt+2G.  Between barriers
+    // the waves read tiles kt+1..kt+G, all covered by this barrier.
+    constexpr int G = C::G, S = C::STAGES;
+#pragma unroll
+    for (int j = 0; j <= G; j++)
+      if (j < nk) dma(j, j);
+    if (nk > G) wait_vmcnt<G * C::kInstr>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    K::read_all(f0, K::at(lds0, off));
+#define VS_GEN6_STEPG(CUR, NXT)                                                 \
+  {                                                                             \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                          \
+    K::template mfma_half<0, false>(acc, CUR, NXT, K::at(0u, off));             \
+    if ((kt & (G - 1)) == 0) {                                                  \
+      wait_vmcnt<0>();                                                          \
+      __builtin_amdgcn_s_barrier();                                             \
+      _Pragma("unroll") for (int j = 1; j <= G; j++) {                          \
+        if (kt + G + j < nk) dma((kt + G + j) & (S - 1), kt + G + j);           \
+      }                                                                         \
+    }                                                                           \
+    const uint32_t sbase = lds0 + ((kt + 1) & (S - 1)) * C::kStage;             \
+    K::template mfma_half<2, true>(acc, CUR, NXT, K::at(sbase, off));           \
+    kt++;                                                                       \
+  }
+    for (int kt = 0; kt < nk;) {
+      VS_GEN6_STEPG(f0, f1)
+      if (kt < nk) VS_GEN6_STEPG(f1, f0)
+    }
+#undef VS_GEN6_STEPG
   }
 #undef VS_GEN6_STEP
 
@@ -685,12 +727,12 @@ __global__ __launch_bounds__(256) void sgemm_splitk_reduce(const float *__restri
 }
 
 // Tile geometry x transposes x DMA width.
-template <int BM, int BN, int WM, int WN, int DMA, bool AGPR, int LDS_KB>
+template <int BM, int BN, int WM, int WN, int DMA, bool AGPR, int LDS_KB, int G = 1>
 bool launch_gen6_t(const GemmArgs &g, int ta, int tb, int batch, hipStream_t s) {
-  if (!ta && !tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, false, false, DMA, AGPR, LDS_KB>>(g, batch, s);
-  if (!ta && tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, false, true, DMA, AGPR, LDS_KB>>(g, batch, s);
-  if (ta && !tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, true, false, DMA, AGPR, LDS_KB>>(g, batch, s);
-  return launch_cfg6<Cfg6<BM, BN, WM, WN, true, true, DMA, AGPR, LDS_KB>>(g, batch, s);
+  if (!ta && !tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, false, false, DMA, AGPR, LDS_KB, G>>(g, batch, s);
+  if (!ta && tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, false, true, DMA, AGPR, LDS_KB, G>>(g, batch, s);
+  if (ta && !tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, true, false, DMA, AGPR, LDS_KB, G>>(g, batch, s);
+  return launch_cfg6<Cfg6<BM, BN, WM, WN, true, true, DMA, AGPR, LDS_KB, G>>(g, batch, s);
 }
 
 // 16-byte DMA needs 16-byte aligned operand rows whose contiguous dimension
@@ -705,7 +747,8 @@ bool gen6_dma16(const GemmArgs &g, int ta, int tb, int batch) {
 // tile: 0 = 128 x 128 (4 waves of 64 x 64), 1 = 256 x 256 (4 waves of
 // 128 x 128, AGPR accumulators), 2 = 64 x 64 (4 waves of 32 x 32),
 // 3 / 4 = 256 x 256 with 8 waves (2 x 4 / 4 x 2, two per SIMD), 5 = 128 x 128
-// with 8 waves (2 x 4); 4-byte DMA
+// with 8 waves (2 x 4), 6 = 2 with an eight-stage ring (64 KiB: two blocks
+// per CU) and a barrier every four k tiles; 4-byte DMA
 // at 128 x 128 / 64 x 64 only (vmcnt range).
 bool launch_gen6_tile(const GemmArgs &g, int ta, int tb, int batch, hipStream_t s, int tile) {
   const bool d16 = gen6_dma16(g, ta, tb, batch);
@@ -715,6 +758,10 @@ bool launch_gen6_tile(const GemmArgs &g, int ta, int tb, int batch, hipStream_t 
   if (tile == 5) {  // 128 x 128 with 8 waves (2 x 4 of 64 x 32)
     if (d16) return launch_gen6_t<128, 128, 2, 4, 16, false, 0>(g, ta, tb, batch, s);
     return launch_gen6_t<128, 128, 2, 4, 4, false, 0>(g, ta, tb, batch, s);
+  }
+  if (tile == 6) {  // 64 x 64, 4 waves, barrier every 4 k tiles (2 otherwise)
+    if (d16) return launch_gen6_t<64, 64, 2, 2, 16, false, 0, 4>(g, ta, tb, batch, s);
+    tile = 2;
   }
   if (tile == 2) {
     if (d16) return launch_gen6_t<64, 64, 2, 2, 16, false, 0>(g, ta, tb, batch, s);
@@ -738,7 +785,7 @@ int auto_splits(long tiles, int k) {
 // partial tiles to a workspace, one reduction pass applying alpha / beta.
 bool launch_gen6(const GemmArgs &g0, int ta, int tb, int batch, hipStream_t s, int tile,
                  int splits = 0) {
-  const int bm = (tile == 1 || tile == 3 || tile == 4) ? 256 : tile == 2 ? 64 : 128;  // 0, 5: 128
+  const int bm = (tile == 1 || tile == 3 || tile == 4) ? 256 : (tile == 2 || tile == 6) ? 64 : 128;
   const long tiles = static_cast<long>((g0.m + bm - 1) / bm) * ((g0.n + bm - 1) / bm) * batch;
   if (splits <= 0) splits = auto_splits(tiles, g0.k);
   if (splits <= 1) {
@@ -799,9 +846,13 @@ int default_variant() {
 // best modelled score wins, larger tiles on ties.  Calibrated on MI355X
 // (profiles/r2/sgemm_w8_ab.md): 256 x 256 8-wave 1 / CU at 1.0, 128 x 128
 // 8-wave 2 / CU at 0.94, 64 x 64 4-wave 4 / CU at 0.90, split-K passes x 0.95.
-// E.g. 4096^3 -> 256 tiles (143 TF); 3072^3 -> 64 x 64 (125 vs 103 TF with
-// 128 x 128); 2048 x 4096 x 2048 -> 128 x 128; 1024 x 1024 x 4096 -> 128 x 128
-// split-K (97 vs 90 TF).
+// When the 64 x 64 blocks (split-K slices included) fit two per CU, the
+// eight-stage, barrier-every-four-tiles build (64 KiB LDS, still two per
+// CU) runs instead: a lone 4-wave block per SIMD set does only 16 MFMAs per
+// wave between barriers at one k tile per barrier (512^3 21.7 -> 22.6,
+// 300 x 1000 x 256 NN / NT 17.2 -> 18.1 / 18.5 -> 19.4 TF, 1000^3 flat; with
+// more blocks than two per CU it loses 6-9 %, the bigger ring stopping
+// blocks from sharing a CU: profiles/r2/session6/sgemm_barrier_cadence.md).
 int pick_variant(int m, int n, int k, int batch) {
   const long cus = device_cu_count();
   const auto eff = [&](long work, long slots) {
@@ -817,7 +868,7 @@ int pick_variant(int m, int n, int k, int batch) {
   const double c = 0.90 * eff(t64 * s64, 4 * cus) * (s64 > 1 ? 0.95 : 1.0);
   if (a >= b && a >= c) return 6;
   if (b >= c) return s128 > 1 ? 9 : 8;
-  return 4;
+  return t64 * s64 <= 2 * cus ? 10 : 4;
 }
 
 vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
@@ -868,6 +919,7 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
       break;
     case 8: ok = launch_gen6(g, ta, tb, batch, s, 5, 1); break;  // 128 x 128, 8 waves
     case 9: ok = launch_gen6(g, ta, tb, batch, s, 5); break;     // same, split-K
+    case 10: ok = launch_gen6(g, ta, tb, batch, s, 6); break;     // 4, barrier / 4 k tiles
     default:
       set_error("vs_sgemm: unknown variant %d (0..%d)", variant, VS_SGEMM_VARIANTS - 1);
       return VS_ERR_INVALID;

@@ -135,14 +135,15 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
                                    vs_stream_t stream);
 
 /// Number of SGEMM kernel variants accepted by vs_sgemm_variant.
-#define VS_SGEMM_VARIANTS 10
+#define VS_SGEMM_VARIANTS 11
 /// Tuning entry point: one explicit SGEMM kernel variant.  Gen 6 (any
 /// transpose, ragged shapes, any alignment): 0: 64x64 tiles, 1: 128x128,
 /// 2: 256x256 (AGPR accumulators), 4: 64x64 with automatic split-K,
 /// 5: 128x128 with automatic split-K; 3: gen 5 256x256 for NN whole tiles
 /// (hand-pipelined LDS-DMA ring), gen 6 256x256 otherwise; 6 / 7: gen 5 with
 /// 8 waves per tile (2 x 4 / 4 x 2, two waves per SIMD), gen 6 otherwise;
-/// 8 / 9: gen 6 128x128 with 8 waves (without / with automatic split-K).
+/// 8 / 9: gen 6 128x128 with 8 waves (without / with automatic split-K);
+/// 10: 4 with an eight-stage ring and one barrier per four k tiles.
 /// vs_sgemm picks by output-tile count (csrc/kernels/sgemm.hip sgemm_impl).
 vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
                            int k, float alpha, const float *a, int64_t lda,
