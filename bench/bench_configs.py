@@ -23,9 +23,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from veles.simd_amd import _lib, ops, parallel  # noqa: E402
+from bench import _device_warm  # noqa: E402  (repo-root bench.py: clock-ramp warm-up)
 
 
 def _timeit(fn, steps, warmup, dist_on):
+    _device_warm(fn, dist_on)
     for _ in range(warmup):
         fn()
     if dist_on:
