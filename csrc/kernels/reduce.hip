@@ -141,29 +141,37 @@ __global__ __launch_bounds__(kBlock) void minmax_pass2(const float2 *__restrict_
   }
 }
 
-// uint8 plane min/max: blocks walk rows, lanes walk 4-byte column groups.
+// uint8 plane min/max: blocks walk rows, lanes walk 16-byte column groups
+// (one uint4 load per step over the 16-aligned middle of a row; scalar head
+// and tail).  4-byte groups ran at 2.2 TB/s on an 8192 x 8192 plane.
+__device__ __forceinline__ void mm_word(unsigned v, unsigned &lo, unsigned &hi) {
+  const unsigned b0 = v & 255u, b1 = (v >> 8) & 255u, b2 = (v >> 16) & 255u, b3 = v >> 24;
+  lo = min(lo, min(min(b0, b1), min(b2, b3)));
+  hi = max(hi, max(max(b0, b1), max(b2, b3)));
+}
+
 __global__ __launch_bounds__(kBlock) void minmax2d_pass1(const uint8_t *__restrict__ src,
                                                          int stride, int w, int h,
                                                          uint2 *__restrict__ partial) {
   unsigned lo = 255, hi = 0;
   for (int y = blockIdx.x; y < h; y += gridDim.x) {
     const uint8_t *row = src + static_cast<size_t>(y) * stride;
-    const int head = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(row) & 3)) & 3);
+    const int head = static_cast<int>((16 - (reinterpret_cast<uintptr_t>(row) & 15)) & 15);
     const int hcount = head < w ? head : w;
     for (int x = threadIdx.x; x < hcount; x += blockDim.x) {
       lo = min(lo, static_cast<unsigned>(row[x]));
       hi = max(hi, static_cast<unsigned>(row[x]));
     }
-    const int nv = (w - hcount) / 4;
-    const uchar4 *r4 = reinterpret_cast<const uchar4 *>(row + hcount);
+    const int nv = (w - hcount) / 16;
+    const uint4 *r16 = reinterpret_cast<const uint4 *>(row + hcount);
     for (int i = threadIdx.x; i < nv; i += blockDim.x) {
-      const uchar4 v = r4[i];
-      lo = min(lo, min(min(static_cast<unsigned>(v.x), static_cast<unsigned>(v.y)),
-                       min(static_cast<unsigned>(v.z), static_cast<unsigned>(v.w))));
-      hi = max(hi, max(max(static_cast<unsigned>(v.x), static_cast<unsigned>(v.y)),
-                       max(static_cast<unsigned>(v.z), static_cast<unsigned>(v.w))));
+      const uint4 v = r16[i];
+      mm_word(v.x, lo, hi);
+      mm_word(v.y, lo, hi);
+      mm_word(v.z, lo, hi);
+      mm_word(v.w, lo, hi);
     }
-    for (int x = hcount + nv * 4 + threadIdx.x; x < w; x += blockDim.x) {
+    for (int x = hcount + nv * 16 + threadIdx.x; x < w; x += blockDim.x) {
       lo = min(lo, static_cast<unsigned>(row[x]));
       hi = max(hi, static_cast<unsigned>(row[x]));
     }
@@ -207,7 +215,17 @@ __global__ __launch_bounds__(kBlock) void minmax2d_pass2(const uint2 *__restrict
 }
 
 // dst = (src - min) / ((max - min) / 2) - 1, same operation order as the
-// scalar reference so results agree to the last bit.
+// scalar reference so results agree to the last bit.  Rows over grid.y;
+// each lane converts 4 pixels per step (one uchar4 load, one float4 store:
+// the wave's stores stay contiguous) over the 4-aligned middle of a row
+// whose destination is 16-byte aligned at the same column, scalar head and
+// tail otherwise.  8192 x 8192: one pixel per lane 1.96 TB/s, this 3.9,
+// 16 pixels per lane (four float4 stores 64 B apart across the wave) 2.8
+// (tools/bench_memops.py, profiles/r2/session6/memops.md).
+__device__ __forceinline__ float norm_px(unsigned v, int lo, float diff, bool flat) {
+  return flat ? 0.f : (static_cast<int>(v) - lo) / diff - 1.0f;
+}
+
 __global__ __launch_bounds__(kBlock) void normalize2d_kernel(
     const uint8_t *__restrict__ src, int sstride, int w, int h,
     const uint8_t *__restrict__ mm, int vmin, int vmax, float *__restrict__ dst,
@@ -216,13 +234,28 @@ __global__ __launch_bounds__(kBlock) void normalize2d_kernel(
   const int hi = mm ? mm[1] : vmax;
   const bool flat = hi == lo;
   const float diff = (hi - lo) / 2.f;
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ts = gridDim.x * blockDim.x;
   for (int y = blockIdx.y; y < h; y += gridDim.y) {
     const uint8_t *srow = src + static_cast<size_t>(y) * sstride;
     float *drow = dst + static_cast<size_t>(y) * dstride;
-    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < w;
-         x += gridDim.x * blockDim.x) {
-      drow[x] = flat ? 0.f : (srow[x] - lo) / diff - 1.0f;
+    // first column where the source is 4-aligned; vectorise only if the
+    // destination is 16-aligned there too
+    int head = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(srow) & 3)) & 3);
+    if (head > w) head = w;
+    const bool vec = (reinterpret_cast<uintptr_t>(drow + head) & 15) == 0;
+    if (!vec) head = w;
+    for (int x = t0; x < head; x += ts) drow[x] = norm_px(srow[x], lo, diff, flat);
+    const int nv = (w - head) / 4;
+    const uchar4 *s4 = reinterpret_cast<const uchar4 *>(srow + head);
+    float4 *d4 = reinterpret_cast<float4 *>(drow + head);
+#pragma unroll 4
+    for (int i = t0; i < nv; i += ts) {
+      const uchar4 v = s4[i];
+      d4[i] = make_float4(norm_px(v.x, lo, diff, flat), norm_px(v.y, lo, diff, flat),
+                          norm_px(v.z, lo, diff, flat), norm_px(v.w, lo, diff, flat));
     }
+    for (int x = head + 4 * nv + t0; x < w; x += ts) drow[x] = norm_px(srow[x], lo, diff, flat);
   }
 }
 
@@ -294,9 +327,14 @@ vs_status vs_normalize2d_u8(const uint8_t *src, int sstride, int w, int h,
   VS_REQUIRE(src && dst && w > 0 && h > 0 && sstride >= w && dstride >= w,
              "vs_normalize2d_u8: invalid arguments");
   VS_REQUIRE(mm || vmin <= vmax, "vs_normalize2d_u8: min > max");
-  const unsigned gx = static_cast<unsigned>((w + kBlock - 1) / kBlock);
+  // rows over grid.y, the row's 4-pixel groups over grid.x (x blocks only as
+  // many as keep ~16 K blocks in flight, so tall images get one per row)
   unsigned gy = static_cast<unsigned>(h);
-  if (gy > 4096) gy = 4096;
+  if (gy > 16384) gy = 16384;
+  unsigned gx = static_cast<unsigned>((w / 4 + kBlock - 1) / kBlock);
+  const unsigned gx_cap = (16384 + gy - 1) / gy;
+  if (gx > gx_cap) gx = gx_cap;
+  if (gx == 0) gx = 1;
   hipLaunchKernelGGL(normalize2d_kernel, dim3(gx, gy), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), src, sstride, w, h, mm,
                      vmin, vmax, dst, dstride);

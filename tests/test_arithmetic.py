@@ -179,3 +179,26 @@ def test_mismatched_alignment_is_accepted():
             fn = getattr(capi._lib.lib(), "int16_to_float")
             fn(capi.p(s), s.size, capi.p(out))
             np.testing.assert_array_equal(out, s.astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,off", [(1 << 20, 0), ((1 << 20) + 3, 0), (4099, 1), (4098, 2), (1, 0)])
+def test_complex_conjugate_device_paths(n, off):
+    """float4 path (16-byte aligned) and scalar path (offset views), odd lengths:
+    pairs conjugated, an odd trailing float left untouched."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    a = torch.randn(n + off, device="cuda")
+    out = torch.full((n + off,), 9.0, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(lib.vs_complex_conjugate(ctypes.c_void_p(a.data_ptr() + 4 * off),
+                                        ctypes.c_void_p(out.data_ptr() + 4 * off), n, s),
+               "vs_complex_conjugate")
+    even = n & ~1
+    want = a[off:off + even].clone()
+    want[1::2] = -want[1::2]
+    assert torch.equal(out[off:off + even], want)
+    if n & 1:
+        assert out[off + n - 1].item() == 9.0

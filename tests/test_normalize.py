@@ -69,3 +69,41 @@ def test_normalize2d_device_large():
     want = (x.float() - mn) / np.float32((mx - mn) / 2.0) - 1.0
     torch.testing.assert_close(got, want, atol=0, rtol=0)
     assert torch.equal(ops.minmax(x.cuda()).cpu(), torch.tensor([mn, mx], dtype=torch.uint8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h,w,sstride,dstride,off", [
+    (37, 1923, 1923, 1923, 0),     # odd width: rows drift in and out of alignment
+    (64, 4096, 4096, 4096, 0),     # every row 16-aligned: all-vector path
+    (50, 1000, 1003, 1001, 3),     # odd strides, source offset 3 bytes
+    (1, 1 << 20, 1 << 20, 1 << 20, 0),  # one wide row: x blocks of the 2-D grid
+    (3000, 5, 7, 6, 1),            # narrow rows: head / tail only
+])
+def test_normalize2d_device_strided(h, w, sstride, dstride, off):
+    """vs_minmax2d_u8 / vs_normalize2d_u8 (16-byte / uchar4 -> float4 paths with
+    scalar heads and tails) against the host formula on strided, offset planes."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(h + w)
+    buf = torch.randint(0, 256, (off + h * sstride + 16,), dtype=torch.uint8, generator=g)
+    x = buf[off:off + h * sstride].reshape(h, sstride)[:, :w]
+    mn, mx = int(x.min()), int(x.max())
+    dbuf = torch.full((h * dstride + 4,), 7.0, device="cuda")
+    src = buf.cuda()
+    mm = torch.empty(2, dtype=torch.uint8, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    sp = ctypes.c_void_p(src.data_ptr() + off)
+    _lib.check(lib.vs_minmax2d_u8(sp, sstride, w, h, ctypes.c_void_p(mm.data_ptr()), s),
+               "vs_minmax2d_u8")
+    assert mm.cpu().tolist() == [mn, mx]
+    # destination offset by one float: a 4-byte aligned, not 16-byte aligned start
+    dp = ctypes.c_void_p(dbuf.data_ptr() + 4)
+    _lib.check(lib.vs_normalize2d_u8(sp, sstride, w, h, ctypes.c_void_p(mm.data_ptr()), 0, 0,
+                                     dp, dstride, s), "vs_normalize2d_u8")
+    got = dbuf.cpu()[1:1 + h * dstride].reshape(h, dstride)
+    want = (x.float() - mn) / np.float32((mx - mn) / 2.0) - 1.0
+    torch.testing.assert_close(got[:, :w], want, atol=0, rtol=0)
+    if dstride > w:
+        assert (got[:, w:] == 7.0).all()
