@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(float *__restrict__ p,
   for (size_t i = done + tid; i < n; i += stride) p[i] = v;
 }
 
-template <bool PAIRS>
+template <bool PAIRS, bool VEC = false>
 __global__ __launch_bounds__(kBlock) void reverse_kernel(
     const float *__restrict__ src, float *__restrict__ dst, size_t n) {
   const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
@@ -326,6 +326,17 @@ __global__ __launch_bounds__(kBlock) void reverse_kernel(
     const float2 *s = reinterpret_cast<const float2 *>(src);
     float2 *d = reinterpret_cast<float2 *>(dst);
     for (size_t i = tid; i < np; i += stride) d[i] = s[np - 1 - i];
+  } else if (VEC) {
+    // dst 16-byte aligned and src + n 16-byte aligned: dst float4 i is the
+    // reversed float4 of src ending at n - 4 i; the last n % 4 outputs come
+    // from src[0 .. n % 4) (3.6 -> ~5.8 TB/s at 2^26, tools/bench_memops.py)
+    const size_t n4 = n / 4;
+    const float4 *s4 = reinterpret_cast<const float4 *>(src + n) - 1;
+    for (size_t i = tid; i < n4; i += stride) {
+      const float4 v = *(s4 - i);
+      reinterpret_cast<float4 *>(dst)[i] = make_float4(v.w, v.z, v.y, v.x);
+    }
+    for (size_t i = 4 * n4 + tid; i < n; i += stride) dst[i] = src[n - 1 - i];
   } else {
     for (size_t i = tid; i < n; i += stride) dst[i] = src[n - 1 - i];
   }
@@ -456,6 +467,9 @@ vs_status vs_reverse(const float *src, float *dst, size_t n, int pairs,
   auto s = static_cast<hipStream_t>(stream);
   if (pairs)
     hipLaunchKernelGGL(reverse_kernel<true>, dim3(elementwise_grid(n / 2, kBlock)),
+                       dim3(kBlock), 0, s, src, dst, n);
+  else if (aligned_to(dst, 16) && aligned_to(src + n, 16))
+    hipLaunchKernelGGL((reverse_kernel<false, true>), dim3(elementwise_grid(n / 4 + 1, kBlock)),
                        dim3(kBlock), 0, s, src, dst, n);
   else
     hipLaunchKernelGGL(reverse_kernel<false>, dim3(elementwise_grid(n, kBlock)),

@@ -202,3 +202,30 @@ def test_complex_conjugate_device_paths(n, off):
     assert torch.equal(out[off:off + even], want)
     if n & 1:
         assert out[off + n - 1].item() == 9.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pairs", [0, 1])
+@pytest.mark.parametrize("n,soff,doff", [(1 << 20, 0, 0), ((1 << 20) + 1, 3, 0),
+                                         ((1 << 20) + 2, 2, 0), (4099, 1, 0), (4100, 0, 1),
+                                         (7, 1, 0), (1, 0, 0)])
+def test_reverse_device_paths(pairs, n, soff, doff):
+    """vs_reverse: the float4 path (dst and src + n 16-byte aligned, n % 4 tail
+    from the front of src), the scalar path, and complex-pair reversal."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    src = torch.randn(n + soff, device="cuda")
+    dst = torch.full((n + doff,), 5.0, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(lib.vs_reverse(ctypes.c_void_p(src.data_ptr() + 4 * soff),
+                              ctypes.c_void_p(dst.data_ptr() + 4 * doff), n, pairs, s),
+               "vs_reverse")
+    x = src[soff:]
+    if pairs:
+        np_ = n // 2
+        want = x[:2 * np_].reshape(np_, 2).flip(0).reshape(-1)
+        assert torch.equal(dst[doff:doff + 2 * np_], want)
+    else:
+        assert torch.equal(dst[doff:], x.flip(0))

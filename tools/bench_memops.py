@@ -39,6 +39,8 @@ def main():
     x = torch.randn(n, device="cuda", generator=g)
     y = torch.randn(n, device="cuda", generator=g)
     z = torch.empty(n, device="cuda")
+    w2 = torch.empty(n, device="cuda")
+    xa = x.abs() + 0.1
     xi16 = (x * 1000).to(torch.int16)
     yi16 = (y * 1000).to(torch.int16)
     oi16 = torch.empty(n, dtype=torch.int16, device="cuda")
@@ -65,6 +67,13 @@ def main():
         "complex multiply": (lambda: chk(lib.vs_complex_multiply(P(x), P(y), P(z), n // 2, 0, s)),
                              12 * n),
         "complex conjugate": (lambda: chk(lib.vs_complex_conjugate(P(x), P(z), n, s)), 8 * n),
+        "reverse": (lambda: chk(lib.vs_reverse(P(x), P(z), n, 0, s)), 8 * n),
+        "reverse complex pairs": (lambda: chk(lib.vs_reverse(P(x), P(z), n, 1, s)), 8 * n),
+        "affine": (lambda: chk(lib.vs_affine(P(x), ctypes.c_float(2.0), ctypes.c_float(1.0),
+                                             P(z), n, s)), 8 * n),
+        "fill": (lambda: chk(lib.vs_fill(P(z), ctypes.c_float(1.5), n, s)), 4 * n),
+        "pow": (lambda: chk(lib.vs_pow(P(xa), P(y), P(z), n, s)), 12 * n),
+        "sincos": (lambda: chk(lib.vs_sincos(P(x), P(z), P(w2), n, s)), 12 * n),
         "int16 multiply": (lambda: chk(lib.vs_int16_multiply(P(xi16), P(yi16), P(oi32), n, s)),
                            8 * n),
         "sum": (lambda: chk(lib.vs_sum(P(x), n, P(out), s)), 4 * n),
