@@ -131,21 +131,44 @@ __global__ __launch_bounds__(kDirThreads) void direct_kernel(
 // Short filters (h <= HM): taps in registers (zero-padded to HM), the x
 // window of the block staged once in LDS, each lane reads its 8 + HM - 1
 // window samples with 16-byte LDS reads.  Memory-bound: one pass over x and y.
-template <int HM>
+// VEC (x rows 16-byte aligned): the window starts at n0 - HM, a multiple of
+// 4 floats, and is filled with float4 loads; the outputs leave through LDS
+// as float4 stores realigned to each row's 16-byte boundaries (the scalar
+// build moved 4 bytes per lane per instruction both ways: h = 4 at 3.2 TB/s,
+// tools/bench_conv.py HLENS=4).
+template <int HM, bool VEC>
 __global__ __launch_bounds__(kDirThreads) void direct_small_kernel(
     const float *__restrict__ x, int xlen, int64_t xs, const float *__restrict__ h,
     int hlen, int64_t hs, float *__restrict__ y, int64_t ys, int ylen, int reverse) {
+  constexpr int SH = VEC ? 1 : 0;      // window offset of x[n0 - (HM - 1)]
   constexpr int W = kDirOut + HM + 8;  // window floats (+ slack for the b128 reads)
+  static_assert(W % 4 == 0, "float4 window");
   __shared__ __attribute__((aligned(16))) float sx[W];
   const int sig = blockIdx.y;
   const float *xrow = x + sig * xs;
   const float *hrow = h + sig * hs;
   const int n0 = blockIdx.x * kDirOut;
-  // window: sx[i] = x[n0 - (HM - 1) + i]
-  const int xbase = n0 - (HM - 1);
-  for (int i = threadIdx.x; i < W; i += kDirThreads) {
-    const int p = xbase + i;
-    sx[i] = (p >= 0 && p < xlen) ? xrow[p] : 0.f;
+  // window: sx[i] = x[n0 - (HM - 1) - SH + i]
+  const int xbase = n0 - (HM - 1) - SH;
+  if (VEC) {
+    for (int i4 = threadIdx.x; i4 < W / 4; i4 += kDirThreads) {
+      const int p = xbase + 4 * i4;
+      float4 v;
+      if (p >= 0 && p + 3 < xlen) {
+        v = *reinterpret_cast<const float4 *>(xrow + p);
+      } else {
+        v.x = (p >= 0 && p < xlen) ? xrow[p] : 0.f;
+        v.y = (p + 1 >= 0 && p + 1 < xlen) ? xrow[p + 1] : 0.f;
+        v.z = (p + 2 >= 0 && p + 2 < xlen) ? xrow[p + 2] : 0.f;
+        v.w = (p + 3 >= 0 && p + 3 < xlen) ? xrow[p + 3] : 0.f;
+      }
+      reinterpret_cast<float4 *>(sx)[i4] = v;
+    }
+  } else {
+    for (int i = threadIdx.x; i < W; i += kDirThreads) {
+      const int p = xbase + i;
+      sx[i] = (p >= 0 && p < xlen) ? xrow[p] : 0.f;
+    }
   }
   float tap[HM];
 #pragma unroll
@@ -153,7 +176,7 @@ __global__ __launch_bounds__(kDirThreads) void direct_small_kernel(
     tap[m] = m < hlen ? (reverse ? hrow[hlen - 1 - m] : hrow[m]) : 0.f;
   __syncthreads();
   const int q0 = threadIdx.x * kDirPerThread;
-  constexpr int NW = (kDirPerThread + HM - 1 + 3) / 4;  // float4 reads per lane
+  constexpr int NW = (kDirPerThread + HM - 1 + SH + 3) / 4;  // float4 reads per lane
   float w[4 * NW];
 #pragma unroll
   for (int c = 0; c < NW; c++) {
@@ -163,16 +186,51 @@ __global__ __launch_bounds__(kDirThreads) void direct_small_kernel(
     w[4 * c + 2] = v.z;
     w[4 * c + 3] = v.w;
   }
-  // y[n0 + q0 + r] = sum_m tap[m] x[n0 + q0 + r - m] = sum_m tap[m] w[r - m + HM - 1]
+  // y[n0 + q0 + r] = sum_m tap[m] x[n0 + q0 + r - m] = sum_m tap[m] w[r - m + HM - 1 + SH]
   float acc[kDirPerThread];
 #pragma unroll
   for (int r = 0; r < kDirPerThread; r++) {
     float a = 0.f;
 #pragma unroll
-    for (int m = 0; m < HM; m++) a = fmaf(tap[m], w[r - m + HM - 1], a);
+    for (int m = 0; m < HM; m++) a = fmaf(tap[m], w[r - m + HM - 1 + SH], a);
     acc[r] = a;
   }
-  store_outputs(acc, sx, y + sig * ys, n0, q0, ylen);
+  float *yrow = y + sig * ys;
+  if (VEC) {
+    __syncthreads();  // every lane is done reading the window
+#pragma unroll
+    for (int r = 0; r < kDirPerThread; r++) sx[q0 + r] = acc[r];
+    __syncthreads();
+    // float4 stores at 16-byte aligned addresses of this row: outputs
+    // n0 + d + 4 g (d = the row's misalignment in floats, n0 % 4 == 0); the
+    // d leading and 4 - d trailing outputs of the block are stored singly
+    const int d = static_cast<int>((4 - ((reinterpret_cast<uintptr_t>(yrow) >> 2) & 3)) & 3);
+    constexpr int G = kDirOut / 4;
+#pragma unroll
+    for (int k = 0; k < kDirPerThread / 4; k++) {
+      const int g = threadIdx.x + k * kDirThreads;
+      const int o = n0 + d + 4 * g;
+      if (d != 0 && g == G - 1) continue;  // reaches into the next block
+      const int b = d + 4 * g;
+      const float4 v = make_float4(sx[b], sx[b + 1], sx[b + 2], sx[b + 3]);
+      if (o + 3 < ylen) {
+        *reinterpret_cast<float4 *>(yrow + o) = v;
+      } else {
+        if (o < ylen) yrow[o] = v.x;
+        if (o + 1 < ylen) yrow[o + 1] = v.y;
+        if (o + 2 < ylen) yrow[o + 2] = v.z;
+      }
+    }
+    if (d != 0 && threadIdx.x < 4) {
+      // head: outputs n0 .. n0 + d - 1; tail: n0 + kDirOut - 4 + d .. n0 + kDirOut - 1
+      const int t = threadIdx.x;
+      if (t < d && n0 + t < ylen) yrow[n0 + t] = sx[t];
+      const int j = kDirOut - 4 + d + t;
+      if (j < kDirOut && n0 + j < ylen) yrow[n0 + j] = sx[j];
+    }
+  } else {
+    store_outputs(acc, sx, yrow, n0, q0, ylen);
+  }
 }
 
 // Small grids (few signals, short outputs, long filters -- e.g. one
@@ -884,9 +942,11 @@ int os_block_log(int hlen) {
 int select(int xlen, int hlen, int batch) {
   const long long ylen = static_cast<long long>(xlen) + hlen - 1;
   (void)batch;
-  // Direct only for very short filters or signals: at x = 2^20 the fused
-  // overlap-save kernel already beats the direct one from h = 16 on
-  // (405 vs 267 Gsamples/s, profiles/r1/conv_sweep_v2.log).
+  // Direct only for very short filters or signals: at x = 2^20 x 64 the
+  // float4 direct kernel runs h <= 8 at ~650 Gsamples/s against ~490 for
+  // overlap-save; at h = 16 they are level (505 vs 500 with 16-byte aligned
+  // rows, 330 without) and from h = 32 overlap-save wins (490 vs 350)
+  // (profiles/r2/session6/conv_small.md).
   if (ylen <= 64 || hlen <= 8 || (hlen <= 32 && xlen < 4096)) return VS_CONV_DIRECT;
   const int los = os_block_log(hlen);
   // Overlap-save while >= 20 % of each block is useful output: the block rule
@@ -912,15 +972,23 @@ vs_status run_direct(int correlate, const float *x, int xlen, int64_t xs,
   const int ylen = xlen + hlen - 1;
   const dim3 grid(static_cast<unsigned>((ylen + kDirOut - 1) / kDirOut),
                   static_cast<unsigned>(batch));
-  if (hlen <= 8)
-    hipLaunchKernelGGL(direct_small_kernel<8>, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
-                       hlen, hs, y, ys, ylen, correlate);
-  else if (hlen <= 16)
-    hipLaunchKernelGGL(direct_small_kernel<16>, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
-                       hlen, hs, y, ys, ylen, correlate);
-  else if (hlen <= 32)
-    hipLaunchKernelGGL(direct_small_kernel<32>, grid, dim3(kDirThreads), 0, s, x, xlen, xs, h,
-                       hlen, hs, y, ys, ylen, correlate);
+  // VEC: x rows 16-byte aligned (float4 window loads); y rows may start
+  // anywhere (the store path realigns per row)
+  const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(y) & 3) == 0 && (batch == 1 || xs % 4 == 0);
+#define VS_DIRECT_SMALL(HM)                                                               \
+  {                                                                                       \
+    if (vec)                                                                              \
+      hipLaunchKernelGGL((direct_small_kernel<HM, true>), grid, dim3(kDirThreads), 0, s, x, \
+                         xlen, xs, h, hlen, hs, y, ys, ylen, correlate);                 \
+    else                                                                                  \
+      hipLaunchKernelGGL((direct_small_kernel<HM, false>), grid, dim3(kDirThreads), 0, s, \
+                         x, xlen, xs, h, hlen, hs, y, ys, ylen, correlate);              \
+  }
+  if (hlen <= 8) VS_DIRECT_SMALL(8)
+  else if (hlen <= 16) VS_DIRECT_SMALL(16)
+  else if (hlen <= 32) VS_DIRECT_SMALL(32)
+#undef VS_DIRECT_SMALL
   else if (hlen <= kSplitMaxTaps &&
            static_cast<int64_t>(grid.x) * batch < 2 * device_cu_count())
     hipLaunchKernelGGL(direct_split_kernel, dim3((ylen + 63) / 64, batch),

@@ -221,3 +221,37 @@ def test_fused_four_step_conv(xlen, hlen, batch, corr):
         y0 = ops.conv1d(x, h, algorithm="fft", correlate=corr)
     scale = y0.abs().max().item()
     assert (y1 - y0).abs().max().item() <= 1e-5 * scale
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hlen", [1, 4, 8, 9, 16, 31, 32])
+@pytest.mark.parametrize("xlen,off", [(5000, 0), (4099, 0), (2048, 1), (7, 0)])
+@pytest.mark.parametrize("correlate", [0, 1])
+@pytest.mark.parametrize("packed", [False, True])
+def test_direct_small_vector_and_scalar_paths(hlen, xlen, off, correlate, packed):
+    """Short-filter direct kernel: float4 window / store path (x rows 16-byte
+    aligned; y rows packed back to back, so each row starts at a different
+    offset inside 16 bytes, or padded) and the scalar path (offset x rows),
+    ragged output tails."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    batch = 3
+    xs = xlen + off + (4 - (xlen + off) % 4) % 4   # row stride keeps alignment iff off == 0
+    ylen = xlen + hlen - 1
+    ys = ylen if packed else ylen + off + (4 - (ylen + off) % 4) % 4
+    xb = torch.randn(batch * xs + off, device="cuda")
+    h = torch.randn(hlen, device="cuda")
+    yb = torch.full((batch * ys + off,), 3.0, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(lib.vs_conv1d(1, correlate, ctypes.c_void_p(xb.data_ptr() + 4 * off), xlen, xs,
+                             ctypes.c_void_p(h.data_ptr()), hlen, 0,
+                             ctypes.c_void_p(yb.data_ptr() + 4 * off), ys, batch, s),
+               "vs_conv1d")
+    x = xb[off:off + batch * xs].reshape(batch, xs)[:, :xlen].double()
+    taps = h.double() if correlate else h.double().flip(0)
+    want = torch.nn.functional.conv1d(x[:, None], taps[None, None], padding=hlen - 1)[:, 0]
+    got = yb[off:off + batch * ys].reshape(batch, ys)
+    assert (got[:, :ylen].double() - want).abs().max().item() < 1e-4
+    assert (got[:, ylen:] == 3.0).all()
