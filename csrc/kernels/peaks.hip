@@ -127,6 +127,113 @@ __global__ __launch_bounds__(kThreads) void emit_kernel(
   }
 }
 
+// Vector variant (x 16-byte aligned): each lane loads one float4 (4
+// consecutive samples) per round, its neighbours' edge samples arrive by
+// lane shuffles (lane 0 / 63 of a wave load the sample across the wave
+// boundary), so every sample is loaded once instead of three times.  Round r
+// of thread t covers samples c0 + 1024 r + 4 t + e, e < 4: positions stay in
+// (round, wave, lane, e) order.  Flags of a lane are a 4-bit set; in-wave
+// ranks come from ballots of the bits of each lane's flag count.
+constexpr int kPer4 = kChunk / (4 * kThreads);  // rounds per block (same chunk)
+
+__device__ __forceinline__ unsigned flags4(const float *__restrict__ x, long long i0,
+                                           long long n, int type) {
+  float4 v;
+  if (i0 + 3 < n) {
+    v = *reinterpret_cast<const float4 *>(x + i0);
+  } else {
+    v.x = i0 < n ? x[i0] : 0.f;
+    v.y = i0 + 1 < n ? x[i0 + 1] : 0.f;
+    v.z = i0 + 2 < n ? x[i0 + 2] : 0.f;
+    v.w = i0 + 3 < n ? x[i0 + 3] : 0.f;
+  }
+  const int lane = threadIdx.x & 63;
+  float prev = __shfl_up(v.w, 1);
+  float next = __shfl_down(v.x, 1);
+  if (lane == 0) prev = i0 >= 1 && i0 - 1 < n ? x[i0 - 1] : 0.f;
+  if (lane == 63) next = i0 + 4 < n ? x[i0 + 4] : 0.f;
+  const float s[6] = {prev, v.x, v.y, v.z, v.w, next};
+  unsigned f = 0;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const long long i = i0 + e;
+    const float c = s[e + 1];
+    const float d1 = c - s[e];
+    const float d2 = c - s[e + 2];
+    const bool p = i >= 1 && i < n - 1 && d1 * d2 > 0.f &&
+                   ((d1 > 0.f && (type & kExtremumTypeMaximum)) ||
+                    (d1 < 0.f && (type & kExtremumTypeMinimum)));
+    f |= p ? (1u << e) : 0u;
+  }
+  return f;
+}
+
+__global__ __launch_bounds__(kThreads) void count4_kernel(
+    const float *__restrict__ x, long long n, int type, unsigned *__restrict__ counts) {
+  __shared__ unsigned wsum[kThreads / 64];
+  const long long c0 = static_cast<long long>(blockIdx.x) * kChunk;
+  unsigned cnt = 0;
+#pragma unroll
+  for (int r = 0; r < kPer4; r++)
+    cnt += __popc(flags4(x, c0 + r * 4 * kThreads + 4 * threadIdx.x, n, type));
+  // wave sum of the per-lane counts
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) wsum[wid] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned s = 0;
+    for (int w = 0; w < kThreads / 64; w++) s += wsum[w];
+    counts[blockIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void emit4_kernel(
+    const float *__restrict__ x, long long n, int type,
+    const unsigned *__restrict__ offsets, int *__restrict__ pos,
+    float *__restrict__ val, unsigned long long cap) {
+  __shared__ unsigned wbase[kPer4][kThreads / 64];
+  const long long c0 = static_cast<long long>(blockIdx.x) * kChunk;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long below = (1ULL << lane) - 1ULL;
+  unsigned f[kPer4], rank[kPer4];
+#pragma unroll
+  for (int r = 0; r < kPer4; r++) {
+    f[r] = flags4(x, c0 + r * 4 * kThreads + 4 * threadIdx.x, n, type);
+    const unsigned c = __popc(f[r]);  // 0..4: three bits
+    const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u),
+                             b2 = __ballot(c & 4u);
+    rank[r] = __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
+    if (lane == 0) wbase[r][wid] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // order: round-major, then wavefront
+    unsigned run = offsets[blockIdx.x];
+    for (int r = 0; r < kPer4; r++)
+      for (int w = 0; w < kThreads / 64; w++) {
+        const unsigned c = wbase[r][w];
+        wbase[r][w] = run;
+        run += c;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kPer4; r++) {
+    unsigned slot = wbase[r][wid] + rank[r];
+    const long long i0 = c0 + r * 4 * kThreads + 4 * threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      if (f[r] & (1u << e)) {
+        if (slot < cap) {
+          pos[slot] = static_cast<int>(i0 + e);
+          val[slot] = x[i0 + e];
+        }
+        slot++;
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace peaks
 }  // namespace vs
@@ -146,12 +253,25 @@ vs_status vs_detect_peaks(const float *x, size_t n, int type, int *pos,
   const long long nb = (static_cast<long long>(n) + peaks::kChunk - 1) / peaks::kChunk;
   DeviceBuffer counts;
   VS_TRY(counts.alloc(nb * sizeof(unsigned), s));
-  hipLaunchKernelGGL(peaks::count_kernel, dim3(static_cast<unsigned>(nb)),
-                     dim3(peaks::kThreads), 0, s, x, static_cast<long long>(n), type,
-                     counts.as<unsigned>());
+  // float4 path for 16-byte aligned x (each sample loaded once, not three
+  // times: 2.1 TB/s before at 2^26, tools/bench_memops.py)
+  const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(peaks::count4_kernel, dim3(static_cast<unsigned>(nb)),
+                       dim3(peaks::kThreads), 0, s, x, static_cast<long long>(n), type,
+                       counts.as<unsigned>());
+  else
+    hipLaunchKernelGGL(peaks::count_kernel, dim3(static_cast<unsigned>(nb)),
+                       dim3(peaks::kThreads), 0, s, x, static_cast<long long>(n), type,
+                       counts.as<unsigned>());
   hipLaunchKernelGGL(peaks::scan_kernel, dim3(1), dim3(1024), 0, s,
                      counts.as<unsigned>(), nb, count);
-  if (cap > 0)
+  if (cap > 0 && vec)
+    hipLaunchKernelGGL(peaks::emit4_kernel, dim3(static_cast<unsigned>(nb)),
+                       dim3(peaks::kThreads), 0, s, x, static_cast<long long>(n), type,
+                       counts.as<unsigned>(), pos, val,
+                       static_cast<unsigned long long>(cap));
+  else if (cap > 0)
     hipLaunchKernelGGL(peaks::emit_kernel, dim3(static_cast<unsigned>(nb)),
                        dim3(peaks::kThreads), 0, s, x, static_cast<long long>(n), type,
                        counts.as<unsigned>(), pos, val,

@@ -37,3 +37,40 @@ def test_random_vs_host(n):
     x = np.round(rng.standard_normal(n) * 4).astype(np.float32)  # plateaus too
     for kind in (1, 2, 3):
         assert capi.detect_peaks(1, x, kind) == capi.detect_peaks(0, x, kind)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [3, 5, 63, 64, 65, 255, 4095, 4096, 4097, 3 * 4096 + 1, (1 << 20) + 5])
+@pytest.mark.parametrize("off", [0, 1])
+def test_device_paths_vs_numpy(n, off):
+    """vs_detect_peaks on the device: float4 kernels (16-byte aligned x: lane
+    shuffles for neighbours, wave-edge loads) and scalar kernels (offset x),
+    every extremum type, chunk / wave boundaries, and a capacity below the
+    count (first `cap` in position order)."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    rng = np.random.default_rng(n + off)
+    xh = np.round(rng.standard_normal(n) * 4).astype(np.float32)  # plateaus too
+    buf = torch.zeros(n + off, device="cuda")
+    buf[off:] = torch.from_numpy(xh).cuda()
+    d1, d2 = xh[1:-1] - xh[:-2], xh[1:-1] - xh[2:]
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for kind in (1, 2, 3):
+        sel = d1 * d2 > 0
+        sel &= ((d1 > 0) & bool(kind & 1)) | ((d1 < 0) & bool(kind & 2))
+        want = np.nonzero(sel)[0] + 1
+        for cap in (len(want), max(len(want) // 3, 1)):
+            pos = torch.full((cap,), -1, dtype=torch.int32, device="cuda")
+            val = torch.zeros(cap, device="cuda")
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            _lib.check(lib.vs_detect_peaks(ctypes.c_void_p(buf.data_ptr() + 4 * off), n, kind,
+                                           ctypes.c_void_p(pos.data_ptr()),
+                                           ctypes.c_void_p(val.data_ptr()), cap,
+                                           ctypes.c_void_p(cnt.data_ptr()), s),
+                       "vs_detect_peaks")
+            assert cnt.item() == len(want)
+            k = min(cap, len(want))
+            assert np.array_equal(pos.cpu().numpy()[:k], want[:k])
+            assert np.array_equal(val.cpu().numpy()[:k], xh[want[:k]])
