@@ -192,7 +192,12 @@ __global__ __launch_bounds__(kThreads) void emit4_kernel(
     const float *__restrict__ x, long long n, int type,
     const unsigned *__restrict__ offsets, int *__restrict__ pos,
     float *__restrict__ val, unsigned long long cap) {
-  __shared__ unsigned wbase[kPer4][kThreads / 64];
+  __shared__ unsigned wbase[kPer4][kThreads / 64], wcnt[kPer4][kThreads / 64];
+  // per-wave staging of one round's results (<= 256 per wave), written out
+  // as one contiguous run per wave (lanes' own slots are up to 4 apart: the
+  // direct stores were scattered)
+  __shared__ int spos[kThreads / 64][4 * 64];
+  __shared__ float sval[kThreads / 64][4 * 64];
   const long long c0 = static_cast<long long>(blockIdx.x) * kChunk;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long below = (1ULL << lane) - 1ULL;
@@ -204,33 +209,40 @@ __global__ __launch_bounds__(kThreads) void emit4_kernel(
     const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u),
                              b2 = __ballot(c & 4u);
     rank[r] = __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
-    if (lane == 0) wbase[r][wid] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    if (lane == 0) wcnt[r][wid] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
   }
   __syncthreads();
   if (threadIdx.x == 0) {  // order: round-major, then wavefront
     unsigned run = offsets[blockIdx.x];
     for (int r = 0; r < kPer4; r++)
       for (int w = 0; w < kThreads / 64; w++) {
-        const unsigned c = wbase[r][w];
         wbase[r][w] = run;
-        run += c;
+        run += wcnt[r][w];
       }
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kPer4; r++) {
-    unsigned slot = wbase[r][wid] + rank[r];
     const long long i0 = c0 + r * 4 * kThreads + 4 * threadIdx.x;
+    unsigned k = rank[r];
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       if (f[r] & (1u << e)) {
-        if (slot < cap) {
-          pos[slot] = static_cast<int>(i0 + e);
-          val[slot] = x[i0 + e];
-        }
-        slot++;
+        spos[wid][k] = static_cast<int>(i0 + e);
+        sval[wid][k] = x[i0 + e];
+        k++;
       }
     }
+    __syncthreads();
+    const unsigned long long base = wbase[r][wid];
+    const unsigned cnt = wcnt[r][wid];
+    for (unsigned j = lane; j < cnt; j += 64) {
+      if (base + j < cap) {
+        pos[base + j] = spos[wid][j];
+        val[base + j] = sval[wid][j];
+      }
+    }
+    __syncthreads();
   }
 }
 
