@@ -16,8 +16,10 @@ LDEXTRA  ?=
 COMMON   := $(OPT) -std=c++17 -fPIC -I. -Iinclude -Wall -Wextra \
             -Wno-unused-parameter -Wno-unused-command-line-argument \
             -DVELES_SIMD_IMPLEMENTATION -fvisibility=hidden
+# -packed-fp32-ops: the compiler emits no v_pk_{add,mul,fma}_f32 (some forms
+# of these have returned wrong results on this hardware pool).
 HIPFLAGS := $(COMMON) -x hip --offload-arch=$(ARCH) \
-            -ffp-contract=fast
+            -ffp-contract=fast -Xclang -target-feature -Xclang -packed-fp32-ops
 CXXFLAGS := $(COMMON) -ffp-contract=off
 
 HIP_SRCS := $(sort $(wildcard csrc/kernels/*.hip))

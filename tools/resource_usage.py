@@ -17,7 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def usage(path):
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", f"-I{REPO}", f"-I{REPO}/include",
            "-DVELES_SIMD_IMPLEMENTATION", "-x", "hip", "--offload-arch=gfx950",
-           "-ffp-contract=fast", "--cuda-device-only", "-c", path, "-o", os.devnull,
+           "-ffp-contract=fast", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "--cuda-device-only", "-c", path, "-o", os.devnull,
            "-Rpass-analysis=kernel-resource-usage"]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
