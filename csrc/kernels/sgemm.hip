@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "csrc/kernels/device.h"
 #include "csrc/runtime/runtime.h"
@@ -684,6 +685,265 @@ __global__ __launch_bounds__(C::kThreads) void sgemm6_kernel(GemmArgs g) {
     }
 }
 
+// Generation 7: gen 6's images and fragment layouts with the issue stream of
+// the steady-state k loop laid out for two waves per SIMD.
+//
+// PMC on gen 5 / 6 put the MFMA pipe at 0.92-0.93 busy where hipBLASLt's
+// kernel reaches 0.98 with the same instruction count.  The idle share sat
+// right behind each tile's barrier: every wave ran the same burst there --
+// three scalar branches, v_readfirstlane + s_mov m0 pairs (the wave id came
+// from threadIdx, which the compiler treats as divergent), 64-bit VALU
+// address adds and all of the tile's LDS-DMA pieces back to back (a piece
+// holds the issuing wave for ~60 cycles) -- and with both waves of a SIMD in
+// lockstep nobody fed the matrix pipe meanwhile.  Here:
+//   * the wave id is made uniform once (readfirstlane), DMA voffsets are
+//     loop invariant and the k advance travels in the instruction's scalar
+//     soffset, so a piece is s_mov m0 + buffer_load ... lds and nothing else;
+//   * full tiles run in a branch-free loop (the last tiles, whose DMAs are
+//     absent or k-masked, run gen 6's generic step);
+//   * the pieces are spread over the MFMA gaps behind the fragment reads;
+//   * with 8 waves, waves 4-7 (the SIMD partners of waves 0-3) run half a
+//     tile out of phase inside each barrier interval: group X does
+//     [reads + DMA + MFMA | MFMA only | barrier], group Y
+//     [MFMA only | reads + DMA + MFMA | barrier], so one partner always has
+//     bare MFMAs to issue while the other sits in an LDS / DMA issue slot.
+//     Every wave still passes the same barriers: b_t, which publishes tile
+//     t + 1 and frees tile t's stage, is X's mid-tile barrier of tile t and
+//     Y's end-of-tile barrier of tile t - 1 (Y passes b_0 in its prologue and
+//     none after its last tile: nk + 1 barriers per wave on either path).
+template <class C>
+struct Gen7 {
+  using K = Gen6<C>;
+  static constexpr int TM = C::TM, TN = C::TN, N = 2 * TM * TN;
+  // MFMA gap (index within the load half) that takes DMA piece j: spread
+  // evenly behind the fragment reads
+  static constexpr int slot(int j) {
+    if (K::kReads + C::kInstr >= N) return N - 1 - (C::kInstr - 1 - j) % N;
+    return K::kReads + (j + 1) * (N - K::kReads) / (C::kInstr + 1);
+  }
+  template <int I, int J, class D>
+  __device__ __forceinline__ static void pieces(const D &d) {
+    if constexpr (J < C::kInstr) {
+      if constexpr (slot(J) == I) d(std::integral_constant<int, J>{});
+      pieces<I, J + 1>(d);
+    }
+  }
+  template <int J, class D>
+  __device__ __forceinline__ static void pieces_all(const D &d) {
+    if constexpr (J < C::kInstr) {
+      d(std::integral_constant<int, J>{});
+      pieces_all<J + 1>(d);
+    }
+  }
+  // MFMAs of k-steps S0, S0 + 1; LOAD: fragment read I of the next tile and
+  // the DMA pieces of gap I follow MFMA I
+  template <int S0, bool LOAD, class D, int I = 0>
+  __device__ __forceinline__ static void half(floatx4 (&acc)[TM][TN], const typename K::Frag &f,
+                                              typename K::Frag &nf, const typename K::Addr &ad,
+                                              const D &d) {
+    if constexpr (I < N) {
+      constexpr int s = S0 + I / (TM * TN), x = (I / TN) % TM, y = I % TN;
+      if constexpr (C::AGPR) VS_MFMA_16X16X4_AGPR(acc[x][y], K::opa(f, x, s), K::opb(f, y, s));
+      else VS_MFMA_16X16X4(acc[x][y], K::opa(f, x, s), K::opb(f, y, s));
+      if constexpr (LOAD && I < K::kReads) K::template read<I>(nf, ad);
+      if constexpr (LOAD) pieces<I, 0>(d);
+      half<S0, LOAD, D, I + 1>(acc, f, nf, ad, d);
+    } else if constexpr (LOAD && I < K::kReads) {
+      K::template read<I>(nf, ad);
+      half<S0, LOAD, D, I + 1>(acc, f, nf, ad, d);
+    }
+  }
+};
+
+template <int SZ>
+__device__ __forceinline__ void buffer_dma_s(__amdgpu_buffer_rsrc_t r, lds_void_t *dst,
+                                             uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (SZ == 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+  else __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 4, voff, soff, 0, 0);
+#endif
+}
+
+// One wave's whole tile; Y selects the wave group's phase (see Gen7).  The
+// two groups are separate instantiations called from a uniform branch, each
+// with its own accumulators from zeroing to store (accumulators live across
+// the branch made the register allocator copy / spill them at the join).
+// Every step issues its kInstr DMA pieces: lanes at or past the end of K --
+// the ragged part of the last tile, and whole tiles past it -- get the
+// out-of-range offset, so they fill their (free) stage with zeros; the
+// counted vmcnt is then the same in every step and the k loop has no branch
+// but its back edge.
+template <class C, bool Y>
+__device__ __forceinline__ void sgemm7_run(const GemmArgs &g, uint8_t *smem7, int wid) {
+  using K = Gen6<C>;
+  using K7 = Gen7<C>;
+  static_assert(C::G == 1, "three-stage ring");
+  constexpr int TM = C::TM, TN = C::TN;
+  const unsigned tiles_n = (g.n + C::BN - 1) / C::BN, tiles_m = (g.m + C::BM - 1) / C::BM;
+  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  unsigned tm, tn;
+  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
+  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
+  const int lane = threadIdx.x & 63;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+
+  const int kb = g.kchunk ? static_cast<int>(blockIdx.y) * g.kchunk : 0;
+  const int kn = g.kchunk ? min(g.kchunk, g.k - kb) : g.k;
+  const float *Ab = g.a + blockIdx.z * g.stride_a + (C::TA ? m0 + kb * g.lda : m0 * g.lda + kb);
+  const float *Bb = g.b + blockIdx.z * g.stride_b + (C::TB ? n0 * g.ldb + kb : n0 + kb * g.ldb);
+  float *Cp = g.c + blockIdx.z * g.stride_c + blockIdx.y * g.split_stride;
+  const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Ab), 0, 0x7fffffff,
+                                                    0x00020000);
+  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Bb), 0, 0x7fffffff,
+                                                    0x00020000);
+  // loop-invariant DMA voffsets (row / column mask folded in) and k positions
+  uint32_t voa[C::kInstrA], vob[C::kInstrB];
+  int kka[C::kInstrA], kkb[C::kInstrB];
+#pragma unroll
+  for (int i = 0; i < C::kInstrA; i++) {
+    const auto sa = K::template src<C::AROWS, C::BM>(wid * C::kInstrA + i, lane, g.lda);
+    voa[i] = m0 + sa.mn < g.m ? sa.off : kDmaOut;
+    kka[i] = sa.kk;
+  }
+#pragma unroll
+  for (int i = 0; i < C::kInstrB; i++) {
+    const auto sb = K::template src<C::BROWS, C::BN>(wid * C::kInstrB + i, lane, g.ldb);
+    vob[i] = n0 + sb.mn < g.n ? sb.off : kDmaOut;
+    kkb[i] = sb.kk;
+  }
+  const uint32_t stride_a = C::AROWS ? 64u : static_cast<uint32_t>(64 * g.lda);
+  const uint32_t stride_b = C::BROWS ? 64u : static_cast<uint32_t>(64 * g.ldb);
+  uint8_t *const wbase_a = smem7 + wid * C::kInstrA * C::kInstrBytes;
+  uint8_t *const wbase_b = smem7 + C::kImgA + wid * C::kInstrB * C::kInstrBytes;
+  const int nk = (kn + C::BK - 1) / C::BK;
+  // DMA piece J of tile kt into stage st
+  const auto piece_of = [&](auto jc, int st, int kt) {
+    constexpr int J = decltype(jc)::value;
+    const int rem = kn - kt * C::BK;        // <= 0 for tiles past the end
+    const int ktc = min(kt, nk - 1);        // keeps soffset inside the operand
+    if constexpr (J < C::kInstrA) {
+      const uint32_t o = kka[J] < rem ? voa[J] : kDmaOut;
+      buffer_dma_s<C::DMA>(ra, (lds_void_t *)(wbase_a + st * C::kStage + J * C::kInstrBytes), o,
+                           ktc * stride_a);
+    } else {
+      constexpr int j = J - C::kInstrA;
+      const uint32_t o = kkb[j] < rem ? vob[j] : kDmaOut;
+      buffer_dma_s<C::DMA>(rb, (lds_void_t *)(wbase_b + st * C::kStage + j * C::kInstrBytes), o,
+                           ktc * stride_b);
+    }
+  };
+  const auto dma_all = [&](int st, int kt) {
+    K7::template pieces_all<0>([&](auto jc) { piece_of(jc, st, kt); });
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      acc[x][y] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (C::AGPR) asm volatile("" : "+a"(acc[x][y]));
+      else asm volatile("" : "+v"(acc[x][y]));
+    }
+  asm volatile("s_nop 7" ::: "memory");  // VALU write -> MFMA srcC read
+
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem7));
+  typename K::Offs off;
+  {
+    const int l16 = lane & 15, q = lane >> 4;
+    off = K::offsets(wm * (C::BM / C::WM) + l16, wn * (C::BN / C::WN) + l16, q);
+  }
+  typename K::Frag f0, f1;
+
+  dma_all(0, 0);
+  dma_all(1, 1);
+  dma_all(2, 2);
+  wait_vmcnt<2 * C::kInstr>();
+  __builtin_amdgcn_s_barrier();
+  K::read_all(f0, K::at(lds0, off));
+  if constexpr (Y) {  // b_0: tile 1 published
+    wait_vmcnt<C::kInstr>();
+    __builtin_amdgcn_s_barrier();
+  }
+
+  const auto nodma = [](auto) {};
+  int sc = 0;  // stage of tile kt
+  // tile kt from registers CUR; reads tile kt + 1 into NXT; DMA of tile kt + 3
+#define VS_GEN7_STEP(CUR, NXT)                                                        \
+  {                                                                                   \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                \
+    K7::template half<0, false>(acc, CUR, NXT, K::at(0u, off), nodma);                \
+    if constexpr (!Y) {                                                               \
+      wait_vmcnt<C::kInstr>();                                                        \
+      __builtin_amdgcn_s_barrier();                                                   \
+    }                                                                                 \
+    const int st = sc, kd = kt + 3;                                                   \
+    sc = sc == 2 ? 0 : sc + 1;                                                        \
+    K7::template half<2, true>(acc, CUR, NXT, K::at(lds0 + sc * C::kStage, off),      \
+                               [&](auto jc) { piece_of(jc, st, kd); });               \
+    kt++;                                                                             \
+    if constexpr (Y) {                                                                \
+      if (kt < nk) {                                                                  \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                            \
+        wait_vmcnt<C::kInstr>();                                                      \
+        __builtin_amdgcn_s_barrier();                                                 \
+      }                                                                               \
+    }                                                                                 \
+  }
+  for (int kt = 0; kt < nk;) {
+    VS_GEN7_STEP(f0, f1)
+    if (kt < nk) VS_GEN7_STEP(f1, f0)
+  }
+#undef VS_GEN7_STEP
+  // zero-fill DMAs of the tiles past the end may still be in flight: LDS
+  // must not be handed to the next block's waves before they land
+  wait_vmcnt<0>();
+
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // MFMA -> VALU read
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      if constexpr (C::AGPR) asm volatile("" : "+a"(acc[x][y]));
+      else asm volatile("" : "+v"(acc[x][y]));
+    }
+  int ln = lane;  // store coordinates recomputed here: no registers held across the loop
+  asm volatile("" : "+v"(ln));
+  const int l16 = ln & 15, q = ln >> 4;
+  const int arow = wm * (C::BM / C::WM) + l16;
+  const int bcol = wn * (C::BN / C::WN) + l16;
+  const bool use_beta = g.beta != 0.f;
+  const bool interior = m0 + C::BM <= g.m && n0 + C::BN <= g.n;
+#pragma unroll
+  for (int x = 0; x < TM; x++)
+#pragma unroll
+    for (int y = 0; y < TN; y++) {
+      const int col = n0 + bcol + 16 * y;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = m0 + arow - l16 + 16 * x + 4 * q + r;
+        if (interior || (row < g.m && col < g.n)) {
+          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+          float v = g.alpha * acc[x][y][r];
+          if (use_beta) v += g.beta * *pc;
+          *pc = v;
+        }
+      }
+    }
+}
+
+template <class C>
+__global__ __launch_bounds__(C::kThreads) void sgemm7_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(1024))) uint8_t smem7[];
+  const int wid = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if constexpr (C::kWaves == 8) {
+    if (wid >= 4) sgemm7_run<C, true>(g, smem7, wid);
+    else sgemm7_run<C, false>(g, smem7, wid);
+  } else {
+    sgemm7_run<C, false>(g, smem7, wid);
+  }
+}
+
 // Whether gen 6 can address this call: every DMA offset of a block below
 // 2^31 bytes relative to its block base.
 template <class C>
@@ -693,17 +953,20 @@ bool gen6_fits(const GemmArgs &g) {
   return g.k > 0 && 4 * (ka + 64) < (1LL << 31) && 4 * (kb + 64) < (1LL << 31);
 }
 
-template <class C>
+template <class C, bool GEN7 = false>
 bool launch_cfg6(const GemmArgs &g, int batch, hipStream_t s) {
   if (!gen6_fits<C>(g)) return false;
+  void (*kern)(GemmArgs);
+  if constexpr (GEN7) kern = &sgemm7_kernel<C>;
+  else kern = &sgemm6_kernel<C>;
   static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(&sgemm6_kernel<C>),
+      reinterpret_cast<const void *>(kern),
       hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);
   (void)attr;
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
   const unsigned splits = g.kchunk ? static_cast<unsigned>((g.k + g.kchunk - 1) / g.kchunk) : 1;
-  hipLaunchKernelGGL(sgemm6_kernel<C>, dim3(tiles, splits, static_cast<unsigned>(batch)),
+  hipLaunchKernelGGL(kern, dim3(tiles, splits, static_cast<unsigned>(batch)),
                      dim3(C::kThreads), C::kLdsBytes, s, g);
   return true;
 }
@@ -727,12 +990,16 @@ __global__ __launch_bounds__(256) void sgemm_splitk_reduce(const float *__restri
 }
 
 // Tile geometry x transposes x DMA width.
-template <int BM, int BN, int WM, int WN, int DMA, bool AGPR, int LDS_KB, int G = 1>
+template <int BM, int BN, int WM, int WN, int DMA, bool AGPR, int LDS_KB, int G = 1,
+          bool GEN7 = false>
 bool launch_gen6_t(const GemmArgs &g, int ta, int tb, int batch, hipStream_t s) {
-  if (!ta && !tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, false, false, DMA, AGPR, LDS_KB, G>>(g, batch, s);
-  if (!ta && tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, false, true, DMA, AGPR, LDS_KB, G>>(g, batch, s);
-  if (ta && !tb) return launch_cfg6<Cfg6<BM, BN, WM, WN, true, false, DMA, AGPR, LDS_KB, G>>(g, batch, s);
-  return launch_cfg6<Cfg6<BM, BN, WM, WN, true, true, DMA, AGPR, LDS_KB, G>>(g, batch, s);
+  if (!ta && !tb)
+    return launch_cfg6<Cfg6<BM, BN, WM, WN, false, false, DMA, AGPR, LDS_KB, G>, GEN7>(g, batch, s);
+  if (!ta && tb)
+    return launch_cfg6<Cfg6<BM, BN, WM, WN, false, true, DMA, AGPR, LDS_KB, G>, GEN7>(g, batch, s);
+  if (ta && !tb)
+    return launch_cfg6<Cfg6<BM, BN, WM, WN, true, false, DMA, AGPR, LDS_KB, G>, GEN7>(g, batch, s);
+  return launch_cfg6<Cfg6<BM, BN, WM, WN, true, true, DMA, AGPR, LDS_KB, G>, GEN7>(g, batch, s);
 }
 
 // 16-byte DMA needs 16-byte aligned operand rows whose contiguous dimension
@@ -752,6 +1019,15 @@ bool gen6_dma16(const GemmArgs &g, int ta, int tb, int batch) {
 // at 128 x 128 / 64 x 64 only (vmcnt range).
 bool launch_gen6_tile(const GemmArgs &g, int ta, int tb, int batch, hipStream_t s, int tile) {
   const bool d16 = gen6_dma16(g, ta, tb, batch);
+  // gen 7 (16-byte DMA only): 7 = 256 x 256 8 waves, 8 = 128 x 128 8 waves,
+  // 9 = 128 x 128 4 waves, 10 = 256 x 256 4 waves
+  if (tile == 7 && d16) return launch_gen6_t<256, 256, 2, 4, 16, true, 0, 1, true>(g, ta, tb, batch, s);
+  if (tile == 8 && d16) return launch_gen6_t<128, 128, 2, 4, 16, false, 0, 1, true>(g, ta, tb, batch, s);
+  if (tile == 9 && d16) return launch_gen6_t<128, 128, 2, 2, 16, false, 0, 1, true>(g, ta, tb, batch, s);
+  if (tile == 10 && d16) return launch_gen6_t<256, 256, 2, 2, 16, true, 0, 1, true>(g, ta, tb, batch, s);
+  if (tile == 7 || tile == 10) tile = 3;
+  if (tile == 8) tile = 5;
+  if (tile == 9) tile = 0;
   if (tile == 1 && d16) return launch_gen6_t<256, 256, 2, 2, 16, true, 0>(g, ta, tb, batch, s);
   if (tile == 3 && d16) return launch_gen6_t<256, 256, 2, 4, 16, true, 0>(g, ta, tb, batch, s);
   if (tile == 4 && d16) return launch_gen6_t<256, 256, 4, 2, 16, true, 0>(g, ta, tb, batch, s);
@@ -785,7 +1061,9 @@ int auto_splits(long tiles, int k) {
 // partial tiles to a workspace, one reduction pass applying alpha / beta.
 bool launch_gen6(const GemmArgs &g0, int ta, int tb, int batch, hipStream_t s, int tile,
                  int splits = 0) {
-  const int bm = (tile == 1 || tile == 3 || tile == 4) ? 256 : (tile == 2 || tile == 6) ? 64 : 128;
+  const int bm = (tile == 1 || tile == 3 || tile == 4 || tile == 7 || tile == 10) ? 256
+                 : (tile == 2 || tile == 6)                                       ? 64
+                                                                                  : 128;
   const long tiles = static_cast<long>((g0.m + bm - 1) / bm) * ((g0.n + bm - 1) / bm) * batch;
   if (splits <= 0) splits = auto_splits(tiles, g0.k);
   if (splits <= 1) {
@@ -899,6 +1177,9 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
   if (variant < 0) variant = default_variant();
   if (variant < 0) variant = pick_variant(m, n, k, batch);
   bool ok = false;
+#ifdef VS_SGEMM_PROBE
+  ok = launch_cfg6<Cfg6<256, 256, 2, VS_SGEMM_PROBE, false, false, 16, true, 0, 1>, true>(g, batch, s);
+#else
   switch (variant) {
     case 0: ok = launch_gen6(g, ta, tb, batch, s, 2, 1); break;   // 64 x 64
     case 1: ok = launch_gen6(g, ta, tb, batch, s, 0, 1); break;   // 128 x 128
@@ -920,10 +1201,15 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
     case 8: ok = launch_gen6(g, ta, tb, batch, s, 5, 1); break;  // 128 x 128, 8 waves
     case 9: ok = launch_gen6(g, ta, tb, batch, s, 5); break;     // same, split-K
     case 10: ok = launch_gen6(g, ta, tb, batch, s, 6); break;     // 4, barrier / 4 k tiles
+    case 11: ok = launch_gen6(g, ta, tb, batch, s, 7, 1); break;  // gen 7 256 x 256, 8 waves
+    case 12: ok = launch_gen6(g, ta, tb, batch, s, 8, 1); break;  // gen 7 128 x 128, 8 waves
+    case 13: ok = launch_gen6(g, ta, tb, batch, s, 9, 1); break;  // gen 7 128 x 128, 4 waves
+    case 14: ok = launch_gen6(g, ta, tb, batch, s, 10, 1); break; // gen 7 256 x 256, 4 waves
     default:
       set_error("vs_sgemm: unknown variant %d (0..%d)", variant, VS_SGEMM_VARIANTS - 1);
       return VS_ERR_INVALID;
   }
+#endif
   VS_REQUIRE(ok, "vs_sgemm: operand spans beyond 2^31 bytes per tile row (m %d n %d k %d)", m,
              n, k);
   VS_HIP(hipGetLastError());

@@ -135,7 +135,7 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
                                    vs_stream_t stream);
 
 /// Number of SGEMM kernel variants accepted by vs_sgemm_variant.
-#define VS_SGEMM_VARIANTS 11
+#define VS_SGEMM_VARIANTS 15
 /// Tuning entry point: one explicit SGEMM kernel variant.  Gen 6 (any
 /// transpose, ragged shapes, any alignment): 0: 64x64 tiles, 1: 128x128,
 /// 2: 256x256 (AGPR accumulators), 4: 64x64 with automatic split-K,

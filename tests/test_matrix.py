@@ -146,7 +146,7 @@ def test_sgemm_autograd():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", list(range(11)))
+@pytest.mark.parametrize("variant", list(range(15)))
 def test_sgemm_every_variant(variant):
     """Every SGEMM kernel variant (include/simd/gpu.h VS_SGEMM_VARIANTS) on
     an aligned NN shape (gen 5's shape) and on ragged / transposed shapes,
@@ -170,8 +170,8 @@ def test_sgemm_every_variant(variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 2, 3, 6, 7, 10])
-@pytest.mark.parametrize("k", [16, 32, 48, 64, 80, 96, 112, 128, 144, 4096])
+@pytest.mark.parametrize("variant", [1, 2, 3, 6, 7, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("k", [16, 32, 48, 64, 80, 96, 112, 128, 144, 4096, 5, 23, 100])
 def test_sgemm_pipeline_depths(variant, k):
     """The LDS-DMA rings at every pipeline depth: 1, 2, 3 and more k tiles
     (prologue / drain paths of the counted-vmcnt schedule), beta != 0."""
