@@ -148,3 +148,14 @@ stamps:
 	    LIBDIR=$(STAMPS_BUILD)/lib LIB=$(STAMPS_BUILD)/lib/libvelessimd.so lib
 
 .PHONY: stamps
+
+# Diagnostic build: timing-only SGEMM ablations (compile-time bits ABLATE=4|8|16 drop
+# the in-loop barriers / DMA pieces / fragment reads of the gen-7 kernel;
+# results are wrong by design).  Not the shipped library.
+ABLATE      ?= 4
+ABLATE_BUILD := build-ablate/$(ABLATE)
+ablate:
+	$(MAKE) BUILD=$(ABLATE_BUILD) OPT="-O3 -DVS_SGEMM_ABLATE=$(ABLATE)" \
+	    LIBDIR=$(ABLATE_BUILD)/lib LIB=$(ABLATE_BUILD)/lib/libvelessimd.so lib
+
+.PHONY: ablate

@@ -135,20 +135,24 @@ vs_status vs_sgemm_strided_batched(int trans_a, int trans_b, int m, int n,
                                    vs_stream_t stream);
 
 /// Number of SGEMM kernel variants accepted by vs_sgemm_variant.
-#define VS_SGEMM_VARIANTS 15
-/// Tuning entry point: one explicit SGEMM kernel variant.  Gen 6 (any
-/// transpose, ragged shapes, any alignment): 0: 64x64 tiles, 1: 128x128,
-/// 2: 256x256 (AGPR accumulators), 4: 64x64 with automatic split-K,
-/// 5: 128x128 with automatic split-K; 3: gen 5 256x256 for NN whole tiles
-/// (hand-pipelined LDS-DMA ring), gen 6 256x256 otherwise; 6 / 7: gen 5 with
-/// 8 waves per tile (2 x 4 / 4 x 2, two waves per SIMD), gen 6 otherwise;
-/// 8 / 9: gen 6 128x128 with 8 waves (without / with automatic split-K);
-/// 10: 4 with an eight-stage ring and one barrier per four k tiles.
-/// vs_sgemm picks by output-tile count (csrc/kernels/sgemm.hip sgemm_impl).
+#define VS_SGEMM_VARIANTS 6
+/// Tuning entry point: one explicit SGEMM tile size (every variant takes any
+/// transpose, ragged shapes and any alignment).  0: 64x64 tiles (4 waves),
+/// 1: 128x128 (8 waves), 2: 256x256 (8 waves, AGPR accumulators; 128x128
+/// when an operand is not 16-byte aligned), each with automatic k slicing of
+/// the tiles that would under-fill the chip; 3..5: the same tiles, whole
+/// tiles only.  vs_sgemm picks tile and slicing from a cost model
+/// (csrc/kernels/sgemm.hip plan_units); VELES_SGEMM_VARIANT forces one.
 vs_status vs_sgemm_variant(int variant, int trans_a, int trans_b, int m, int n,
                            int k, float alpha, const float *a, int64_t lda,
                            const float *b, int64_t ldb, float beta, float *c,
                            int64_t ldc, vs_stream_t stream);
+vs_status vs_sgemm_variant_batched(int variant, int trans_a, int trans_b, int m,
+                                   int n, int k, float alpha, const float *a,
+                                   int64_t lda, int64_t stride_a, const float *b,
+                                   int64_t ldb, int64_t stride_b, float beta,
+                                   float *c, int64_t ldc, int64_t stride_c,
+                                   int batch, vs_stream_t stream);
 
 /// bf16 matrix-core GEMM: C (fp32) = alpha op(A) op(B) + beta C with A, B
 /// bf16 (raw uint16 bit patterns), fp32 accumulation (v_mfma_f32_32x32x16_bf16).

@@ -1,4 +1,4 @@
-"""Generation-6 SGEMM (csrc/kernels/sgemm.hip sgemm6_kernel): every
+"""The SGEMM kernel family (csrc/kernels/sgemm.hip sgemm_kernel): every
 transpose combination, ragged M / N / K (buffer LDS-DMA whose out-of-range
 lanes read zeros), 16- and 4-byte DMA, beta, batches and every pipeline
 depth, against float64.  Reference: /root/reference/src/matrix.c:255-343
@@ -9,9 +9,9 @@ import ctypes
 import pytest
 
 pytestmark = pytest.mark.gpu
-# 1: 128 x 128 tiles, 2: 256 x 256 (AGPR accumulators), 0: 64 x 64,
-# 5 / 4: 128 x 128 / 64 x 64 with automatic split-K (workspace + reduction)
-VARIANTS = [0, 1, 2, 4, 5]
+# 0 / 1 / 2: 64 x 64, 128 x 128, 256 x 256 tiles with automatic k slicing
+# (workspace + reduction), 3 / 4 / 5: the same, whole tiles only
+VARIANTS = [0, 1, 2, 3, 4, 5]
 
 
 def _run(variant, m, n, k, ta, tb, lda_pad=0, ldb_pad=0, alpha=1.0, beta=0.0, seed=0,
@@ -78,7 +78,7 @@ def test_gen6_batched(variant):
     assert (c.double() - ref).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 1)])
 def test_gen6_split_k(variant, ta, tb):
     """Deep K on few output tiles: split into >= 256-deep slices, reduced
@@ -103,3 +103,36 @@ def test_k_zero_scales_c(ta, tb):
     _lib.check(lib.vs_sgemm(ta, tb, 37, 53, 0, 1.0, a.data_ptr(), 37 if ta else 1,
                             a.data_ptr(), 1 if tb else 53, 0.0, c.data_ptr(), 53, s), "vs_sgemm")
     assert (c == 0).all()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0)])
+def test_tail_tiles_sliced(variant, ta, tb):
+    """More tiles than CUs with a remainder: the whole tiles run first, the
+    remainder is cut into k slices (partials in a workspace, reduced with
+    alpha / beta applied once).  Ragged edges fall into sliced tiles."""
+    dim = (64, 128, 256)[variant]
+    # 17 x 17 = 289 tiles on 256 CUs -> 33 sliced; the last row / column ragged
+    m = n = 16 * dim + dim // 2 + 4
+    _run(variant, m, n, 384, ta, tb, alpha=0.75, beta=0.5, seed=variant)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_batched_units(variant):
+    """Strided batches: few tiles per matrix (sliced, per-batch workspace
+    slabs) and many (whole tiles)."""
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for (bt, m, n, k) in [(3, 200, 136, 1024), (5, 384, 520, 96)]:
+        g = torch.Generator(device="cuda").manual_seed(bt)
+        a = torch.rand(bt, m, k, device="cuda", generator=g) - 0.5
+        b = torch.rand(bt, k, n, device="cuda", generator=g) - 0.5
+        c = torch.rand(bt, m, n, device="cuda", generator=g)
+        ref = 1.5 * torch.bmm(a.double(), b.double()) - 0.5 * c.double()
+        _lib.check(lib.vs_sgemm_variant_batched(variant, 0, 0, m, n, k, 1.5, a.data_ptr(), k,
+                                                m * k, b.data_ptr(), n, k * n, -0.5,
+                                                c.data_ptr(), n, m * n, bt, s),
+                   "vs_sgemm_variant_batched")
+        assert (c.double() - ref).abs().max().item() < 2e-6 * k + 1e-5, (variant, bt, m, n, k)

