@@ -60,7 +60,7 @@ $(TEST_BIN): tests/native/capi_test.cpp $(LIB) $(HEADERS)
 clean:
 	rm -rf $(BUILD) $(LIB)
 
-# Install: library + the 18 public headers + pkg-config file, the layout of
+# Install: library + the public headers + pkg-config file, the layout of
 # the reference's `make install` (/root/reference/inc/Makefile.am:27-31,
 # src/Makefile.am:29, Simd.pc.in).  The library is also installed as
 # libSimd.so and the .pc as Simd.pc, so `pkg-config --cflags --libs Simd`

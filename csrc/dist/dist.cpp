@@ -583,7 +583,9 @@ vs_status vs_dist_sgemm_rowsplit_device(vs_dist_t c, int m, int n, int k,
   std::vector<size_t> rb(R), rc(R);
   for (int r = 0; r < R; r++) vs_dist_shard(m, R, r, &rb[r], &rc[r]);
   for (int r = 0; r < R; r++)
-    VS_REQUIRE(A[r] && B[r] && C[r], "vs_dist_sgemm_rowsplit_device: rank %d null pointer", r);
+    // a rank that owns no rows (m < ranks) has nothing to read from A
+    VS_REQUIRE((A[r] || rc[r] == 0) && B[r] && C[r],
+               "vs_dist_sgemm_rowsplit_device: rank %d null pointer", r);
   const size_t kn = static_cast<size_t>(k) * n, mn = static_cast<size_t>(m) * n;
   // matrix b: each rank writes its rows into its own full C, then the row
   // blocks are all-gathered in place on the side stream while the next

@@ -15,6 +15,7 @@
 
 #include "csrc/kernels/device.h"
 #include "csrc/runtime/runtime.h"
+#include "simd/device_math.h"
 #include "simd/gpu.h"
 
 namespace vs {
@@ -179,35 +180,17 @@ struct SaxpyOp {
   __device__ float operator()(float x, float y) const { return fmaf(a, x, y); }
 };
 
-// exp(x) with a two-constant (Cody-Waite) reduction x = n ln2 + r and a
-// degree-7 polynomial on |r| <= ln2/2, then ldexp: <= 1 ulp over the whole
-// range.  (A plain exp2(x * log2 e) loses ~|x| * 2^-24 relative accuracy in
-// the product, i.e. up to ~40 ulp near x = 88.)
-__device__ __forceinline__ float accurate_expf(float x) {
-  if (!(x < 88.72283935546875f)) return x != x ? x : __builtin_inff();
-  if (x < -103.97208404541015625f) return 0.f;
-  const float n = rintf(x * 1.44269504088896341f);
-  float r = fmaf(n, -0.693145751953125f, x);
-  r = fmaf(n, -1.428606765330187045e-6f, r);
-  float p = 1.98412698412698413e-4f;
-  p = fmaf(p, r, 1.38888888888888889e-3f);
-  p = fmaf(p, r, 8.33333333333333333e-3f);
-  p = fmaf(p, r, 4.16666666666666667e-2f);
-  p = fmaf(p, r, 1.66666666666666667e-1f);
-  p = fmaf(p, r, 0.5f);
-  p = fmaf(p, r, 1.0f);
-  p = fmaf(p, r, 1.0f);
-  return ldexpf(p, static_cast<int>(n));
-}
-
+// The element functions are the public device-callable ones
+// (include/simd/device_math.h), so user kernels compose exactly what the
+// array kernels run.
 template <int FN>
 struct MathOp {
   __device__ float operator()(float x) const {
-    if constexpr (FN == VS_FN_SIN) return sinf(x);
-    if constexpr (FN == VS_FN_COS) return cosf(x);
-    if constexpr (FN == VS_FN_LOG) return logf(x);
-    if constexpr (FN == VS_FN_SQRT) return sqrtf(x);  // correctly rounded
-    return accurate_expf(x);
+    if constexpr (FN == VS_FN_SIN) return simd_sin_ps(x);
+    if constexpr (FN == VS_FN_COS) return simd_cos_ps(x);
+    if constexpr (FN == VS_FN_LOG) return simd_log_ps(x);
+    if constexpr (FN == VS_FN_SQRT) return simd_sqrt_ps(x);
+    return simd_exp_ps(x);
   }
 };
 // x^y evaluated in double and rounded once: OCML powf was measured at up
@@ -216,7 +199,7 @@ struct MathOp {
 // reaches (12 bytes per element).
 struct PowOp {
   __device__ float operator()(float x, float y) const {
-    return static_cast<float>(pow(static_cast<double>(x), static_cast<double>(y)));
+    return simd_pow_ps(x, y);
   }
 };
 
@@ -231,14 +214,11 @@ __global__ __launch_bounds__(kBlock) void sincos_kernel(const float *__restrict_
   for (size_t i = tid; i < nv; i += stride) {
     const float4 v = reinterpret_cast<const float4 *>(x)[i];
     float4 sv, cv;
-    sincosf(v.x, &sv.x, &cv.x);
-    sincosf(v.y, &sv.y, &cv.y);
-    sincosf(v.z, &sv.z, &cv.z);
-    sincosf(v.w, &sv.w, &cv.w);
+    simd_sincos_ps4(v, &sv, &cv);
     reinterpret_cast<float4 *>(s)[i] = sv;
     reinterpret_cast<float4 *>(c)[i] = cv;
   }
-  for (size_t i = 4 * nv + tid; i < n; i += stride) sincosf(x[i], s + i, c + i);
+  for (size_t i = 4 * nv + tid; i < n; i += stride) simd_sincos_ps(x[i], s + i, c + i);
 }
 
 __global__ __launch_bounds__(kBlock) void sincos_scalar_kernel(const float *__restrict__ x,
@@ -246,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void sincos_scalar_kernel(const float *__re
                                                                float *__restrict__ c, size_t n) {
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n; i += stride)
-    sincosf(x[i], s + i, c + i);
+    simd_sincos_ps(x[i], s + i, c + i);
 }
 
 // ------------------------------------------------------- complex kernels

@@ -11,6 +11,8 @@
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cfloat>
 #include <cstdint>
 
@@ -150,9 +152,12 @@ __device__ __forceinline__ void mm_word(unsigned v, unsigned &lo, unsigned &hi) 
   hi = max(hi, max(max(b0, b1), max(b2, b3)));
 }
 
+// Planes over grid.y (plane stride `pstride` bytes), partial[plane][block].
 __global__ __launch_bounds__(kBlock) void minmax2d_pass1(const uint8_t *__restrict__ src,
-                                                         int stride, int w, int h,
-                                                         uint2 *__restrict__ partial) {
+                                                         int stride, int64_t pstride, int w,
+                                                         int h, uint2 *__restrict__ partial) {
+  src += blockIdx.y * pstride;
+  partial += static_cast<size_t>(blockIdx.y) * gridDim.x;
   unsigned lo = 255, hi = 0;
   for (int y = blockIdx.x; y < h; y += gridDim.x) {
     const uint8_t *row = src + static_cast<size_t>(y) * stride;
@@ -192,6 +197,8 @@ __global__ __launch_bounds__(kBlock) void minmax2d_pass1(const uint8_t *__restri
 
 __global__ __launch_bounds__(kBlock) void minmax2d_pass2(const uint2 *__restrict__ partial,
                                                          int np, uint8_t *__restrict__ out) {
+  partial += static_cast<size_t>(blockIdx.x) * np;  // one block per plane
+  out += 2 * blockIdx.x;
   __shared__ unsigned slo[kBlock], shi[kBlock];
   unsigned lo = 255, hi = 0;
   for (int i = threadIdx.x; i < np; i += blockDim.x) {
@@ -227,11 +234,14 @@ __device__ __forceinline__ float norm_px(unsigned v, int lo, float diff, bool fl
 }
 
 __global__ __launch_bounds__(kBlock) void normalize2d_kernel(
-    const uint8_t *__restrict__ src, int sstride, int w, int h,
+    const uint8_t *__restrict__ src, int sstride, int64_t splane, int w, int h,
     const uint8_t *__restrict__ mm, int vmin, int vmax, float *__restrict__ dst,
-    int dstride) {
-  const int lo = mm ? mm[0] : vmin;
-  const int hi = mm ? mm[1] : vmax;
+    int dstride, int64_t dplane) {
+  // planes over grid.z, each with its own {min, max} pair
+  src += blockIdx.z * splane;
+  dst += blockIdx.z * dplane;
+  const int lo = mm ? mm[2 * blockIdx.z] : vmin;
+  const int hi = mm ? mm[2 * blockIdx.z + 1] : vmax;
   const bool flat = hi == lo;
   const float diff = (hi - lo) / 2.f;
   const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -304,19 +314,69 @@ vs_status vs_minmax(const float *x, size_t n, float *out, vs_stream_t stream) {
   return VS_OK;
 }
 
+vs_status vs_minmax2d_u8_batched(const uint8_t *src, int stride, int64_t plane_stride, int w,
+                                 int h, int planes, uint8_t *out, vs_stream_t stream) {
+  VS_REQUIRE(src && out && w > 0 && h > 0 && stride >= w && planes >= 0,
+             "vs_minmax2d_u8: invalid arguments (w=%d h=%d stride=%d planes=%d)", w, h,
+             stride, planes);
+  VS_REQUIRE(planes <= 1 || plane_stride >= static_cast<int64_t>(stride) * (h - 1) + w,
+             "vs_minmax2d_u8: plane stride smaller than a plane");
+  if (planes == 0) return VS_OK;
+  if (planes > kMaxGridY)
+    return batch_chunks(planes, [&](long long p0, int np) {
+      return vs_minmax2d_u8_batched(src + p0 * plane_stride, stride, plane_stride, w, h, np,
+                                    out + 2 * p0, stream);
+    });
+  auto s = static_cast<hipStream_t>(stream);
+  // blocks per plane: all rows of a lone plane, fewer when many planes
+  // already fill the chip
+  unsigned g = static_cast<unsigned>(h < static_cast<int>(kMaxPartials) ? h : kMaxPartials);
+  const unsigned per_plane = std::max(1u, 16384u / static_cast<unsigned>(planes));
+  if (planes > 1 && g > per_plane) g = per_plane;
+  DeviceBuffer part;
+  VS_TRY(part.alloc(static_cast<size_t>(g) * planes * sizeof(uint2), s));
+  hipLaunchKernelGGL(minmax2d_pass1, dim3(g, static_cast<unsigned>(planes)), dim3(kBlock), 0, s,
+                     src, stride, plane_stride, w, h, part.as<uint2>());
+  hipLaunchKernelGGL(minmax2d_pass2, dim3(static_cast<unsigned>(planes)), dim3(kBlock), 0, s,
+                     part.as<uint2>(), static_cast<int>(g), out);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
+}
+
 vs_status vs_minmax2d_u8(const uint8_t *src, int stride, int w, int h,
                          uint8_t *out, vs_stream_t stream) {
-  VS_REQUIRE(src && out && w > 0 && h > 0 && stride >= w,
-             "vs_minmax2d_u8: invalid arguments (w=%d h=%d stride=%d)", w, h,
-             stride);
-  auto s = static_cast<hipStream_t>(stream);
-  const unsigned g = static_cast<unsigned>(h < static_cast<int>(kMaxPartials) ? h : kMaxPartials);
-  DeviceBuffer part;
-  VS_TRY(part.alloc(g * sizeof(uint2), s));
-  hipLaunchKernelGGL(minmax2d_pass1, dim3(g), dim3(kBlock), 0, s, src, stride, w,
-                     h, part.as<uint2>());
-  hipLaunchKernelGGL(minmax2d_pass2, dim3(1), dim3(kBlock), 0, s,
-                     part.as<uint2>(), static_cast<int>(g), out);
+  return vs_minmax2d_u8_batched(src, stride, 0, w, h, 1, out, stream);
+}
+
+vs_status vs_normalize2d_u8_batched(const uint8_t *src, int sstride, int64_t splane, int w,
+                                    int h, int planes, const uint8_t *mm, int vmin, int vmax,
+                                    float *dst, int dstride, int64_t dplane,
+                                    vs_stream_t stream) {
+  VS_REQUIRE(src && dst && w > 0 && h > 0 && sstride >= w && dstride >= w && planes >= 0,
+             "vs_normalize2d_u8: invalid arguments");
+  VS_REQUIRE(mm || vmin <= vmax, "vs_normalize2d_u8: min > max");
+  VS_REQUIRE(planes <= 1 || (splane >= static_cast<int64_t>(sstride) * (h - 1) + w &&
+                             dplane >= static_cast<int64_t>(dstride) * (h - 1) + w),
+             "vs_normalize2d_u8: plane stride smaller than a plane");
+  if (planes == 0) return VS_OK;
+  if (planes > kMaxGridY)
+    return batch_chunks(planes, [&](long long p0, int np) {
+      return vs_normalize2d_u8_batched(src + p0 * splane, sstride, splane, w, h, np,
+                                       mm ? mm + 2 * p0 : nullptr, vmin, vmax, dst + p0 * dplane,
+                                       dstride, dplane, stream);
+    });
+  // rows over grid.y, the row's 4-pixel groups over grid.x (x blocks only as
+  // many as keep ~16 K blocks in flight, so tall images get one per row),
+  // planes over grid.z
+  unsigned gy = static_cast<unsigned>(h);
+  if (gy > 16384) gy = 16384;
+  unsigned gx = static_cast<unsigned>((w / 4 + kBlock - 1) / kBlock);
+  const unsigned gx_cap = (16384 + gy - 1) / gy;
+  if (gx > gx_cap) gx = gx_cap;
+  if (gx == 0) gx = 1;
+  hipLaunchKernelGGL(normalize2d_kernel, dim3(gx, gy, static_cast<unsigned>(planes)), dim3(kBlock),
+                     0, static_cast<hipStream_t>(stream), src, sstride, splane, w, h, mm, vmin,
+                     vmax, dst, dstride, dplane);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
@@ -324,22 +384,8 @@ vs_status vs_minmax2d_u8(const uint8_t *src, int stride, int w, int h,
 vs_status vs_normalize2d_u8(const uint8_t *src, int sstride, int w, int h,
                             const uint8_t *mm, int vmin, int vmax, float *dst,
                             int dstride, vs_stream_t stream) {
-  VS_REQUIRE(src && dst && w > 0 && h > 0 && sstride >= w && dstride >= w,
-             "vs_normalize2d_u8: invalid arguments");
-  VS_REQUIRE(mm || vmin <= vmax, "vs_normalize2d_u8: min > max");
-  // rows over grid.y, the row's 4-pixel groups over grid.x (x blocks only as
-  // many as keep ~16 K blocks in flight, so tall images get one per row)
-  unsigned gy = static_cast<unsigned>(h);
-  if (gy > 16384) gy = 16384;
-  unsigned gx = static_cast<unsigned>((w / 4 + kBlock - 1) / kBlock);
-  const unsigned gx_cap = (16384 + gy - 1) / gy;
-  if (gx > gx_cap) gx = gx_cap;
-  if (gx == 0) gx = 1;
-  hipLaunchKernelGGL(normalize2d_kernel, dim3(gx, gy), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), src, sstride, w, h, mm,
-                     vmin, vmax, dst, dstride);
-  VS_HIP(hipGetLastError());
-  return VS_OK;
+  return vs_normalize2d_u8_batched(src, sstride, 0, w, h, 1, mm, vmin, vmax, dst, dstride, 0,
+                                   stream);
 }
 
 }  // extern "C"

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -178,8 +179,13 @@ static bool sync_stage() {
 // kernels of a call sequence put a ~6 us gap into the queue (rocprofv3 trace
 // of the conv filter / block kernels, profiles/r2/conv/alloc_gap.md), and
 // the stream handle is only compared, never passed to the runtime, so a
-// stream the caller has since destroyed is harmless.  The out-of-memory
-// purge synchronises the device before freeing.  (The HIP
+// stream the caller has since destroyed is harmless -- provided no new
+// stream is handed the destroyed stream's handle while work of the old one
+// that uses a cached block is still queued (hipStreamDestroy returns before
+// that work ends): a host that destroys streams with library calls still in
+// flight must synchronise them first.  The out-of-memory purge synchronises
+// the device before freeing, and so does the trim that keeps the cached
+// bytes under VELES_SCRATCH_CACHE_MB.  (The HIP
 // stream-ordered pool -- hipMallocAsync -- returned stale results on ROCm 7.2
 // after block reuse in our C API tests; this pool avoids depending on it.)
 class ScratchPool {
@@ -216,6 +222,7 @@ class ScratchPool {
         if (b.stream != stream) continue;
         void *p = b.ptr;
         live_[p] = b;
+        cached_ -= b.size;
         free_.erase(it);
         return p;
       }
@@ -230,7 +237,7 @@ class ScratchPool {
       }
     }
     std::lock_guard<std::mutex> lock(mu_);
-    live_[p] = Block{p, sz, dev, stream};
+    live_[p] = Block{p, sz, dev, stream, 0};
     return p;
   }
 
@@ -245,7 +252,37 @@ class ScratchPool {
     Block b = it->second;
     live_.erase(it);
     b.stream = stream;
+    b.tick = ++tick_;
     free_.emplace(b.size, b);
+    cached_ += b.size;
+    if (cached_ > cap_bytes()) trim_locked();
+  }
+
+  // Cached bytes above the cap (a host that cycles through many streams
+  // builds one cache per stream): synchronise once, then free the blocks
+  // released longest ago until half the cap is left.
+  void trim_locked() {
+    (void)hipDeviceSynchronize();
+    std::vector<std::multimap<size_t, Block>::iterator> order;
+    for (auto it = free_.begin(); it != free_.end(); ++it) order.push_back(it);
+    std::sort(order.begin(), order.end(),
+              [](const auto &a, const auto &b) { return a->second.tick < b->second.tick; });
+    for (auto it : order) {
+      if (cached_ <= cap_bytes() / 2) break;
+      cached_ -= it->second.size;
+      (void)hipFree(it->second.ptr);
+      free_.erase(it);
+    }
+  }
+
+  static size_t cap_bytes() {
+    static const size_t v = static_cast<size_t>(env_int("VELES_SCRATCH_CACHE_MB", 8192)) << 20;
+    return v;
+  }
+
+  size_t cached_bytes() {
+    std::lock_guard<std::mutex> lock(mu_);
+    return cached_;
   }
 
   void release_all_free() {
@@ -253,6 +290,7 @@ class ScratchPool {
     if (!free_.empty()) (void)hipDeviceSynchronize();
     for (auto &kv : free_) (void)hipFree(kv.second.ptr);
     free_.clear();
+    cached_ = 0;
   }
 
  private:
@@ -261,6 +299,7 @@ class ScratchPool {
     size_t size;
     int device;
     hipStream_t stream;
+    uint64_t tick = 0;  // release order (trim_locked frees the oldest first)
   };
   static size_t round(size_t b) {
     if (b <= (1u << 20)) {
@@ -283,6 +322,8 @@ class ScratchPool {
   std::multimap<size_t, Block> free_;
   std::map<void *, Block> live_;
   std::set<void *> graph_;  // captured (graph-owned) allocations
+  size_t cached_ = 0;       // bytes in free_
+  uint64_t tick_ = 0;
 };
 
 vs_status DeviceBuffer::alloc(size_t bytes, hipStream_t stream) {
@@ -426,11 +467,22 @@ vs_status wait_stream(hipStream_t s) {
     ev_dev = dev;
   }
   VS_HIP(hipEventRecord(ev, s));
+  // Short calls (the common host-API case, ~10 us) are caught by polling: a
+  // blocking wait adds the wake-up latency of the interrupt path.  Past
+  // kSpinUs the call is long enough not to care, and a blocking wait frees
+  // the core for other host threads.
+  constexpr long kSpinUs = 50;
+  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipEventQuery(ev);
     if (e == hipSuccess) return VS_OK;
     if (e != hipErrorNotReady) return hip_status(e, "hipEventQuery", __FILE__, __LINE__);
+    const auto us = std::chrono::duration_cast<std::chrono::microseconds>(
+                        std::chrono::steady_clock::now() - t0).count();
+    if (us > kSpinUs) break;
   }
+  VS_HIP(hipEventSynchronize(ev));
+  return VS_OK;
 }
 
 Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)

@@ -104,6 +104,11 @@ vs_status vs_pow(const float *x, const float *y, float *out, size_t n,
 /// avx_mathfun.h:571 sincos256_ps, neon_mathfun.h:228 sincos_ps).
 vs_status vs_sincos(const float *x, float *s, float *c, size_t n,
                     vs_stream_t stream);
+/// Consumer of <simd/device_math.h> (csrc/kernels/device_math_user.hip, a
+/// kernel that includes only that header): morlet[i] = exp(-t^2 / 2)
+/// cos(omega t), feature[i] = log(1 + sqrt(|t|^p)).
+vs_status vs_device_math_example(const float *t, float omega, float p, size_t n,
+                                 float *morlet, float *feature, vs_stream_t stream);
 
 /* ------------------------------------------------------------ reductions */
 /// *out_dev = sum(x) (pairwise tree in fp32).
@@ -113,12 +118,26 @@ vs_status vs_minmax(const float *x, size_t n, float *out_dev,
                     vs_stream_t stream);
 vs_status vs_minmax2d_u8(const uint8_t *src, int src_stride, int width,
                          int height, uint8_t *out_dev, vs_stream_t stream);
+/// `planes` planes `plane_stride` bytes apart in one launch sequence:
+/// out_dev[2 p] = min, out_dev[2 p + 1] = max of plane p.
+vs_status vs_minmax2d_u8_batched(const uint8_t *src, int src_stride,
+                                 int64_t plane_stride, int width, int height,
+                                 int planes, uint8_t *out_dev, vs_stream_t stream);
 /// If minmax_dev != NULL the bounds are read from it (fused normalize2D),
 /// otherwise (vmin, vmax) are used.
 vs_status vs_normalize2d_u8(const uint8_t *src, int src_stride, int width,
                             int height, const uint8_t *minmax_dev, int vmin,
                             int vmax, float *dst, int dst_stride,
                             vs_stream_t stream);
+/// `planes` planes in one launch; minmax_dev (if not NULL) holds one {min,
+/// max} pair per plane (vs_minmax2d_u8_batched), so a stack of images is
+/// normalised plane by plane without a host round trip (reference
+/// src/normalize.c:445-503, one plane per call).
+vs_status vs_normalize2d_u8_batched(const uint8_t *src, int src_stride,
+                                    int64_t src_plane_stride, int width, int height,
+                                    int planes, const uint8_t *minmax_dev, int vmin,
+                                    int vmax, float *dst, int dst_stride,
+                                    int64_t dst_plane_stride, vs_stream_t stream);
 
 /* ------------------------------------------------------------------ GEMM */
 /// C = alpha * op(A) * op(B) + beta * C, row-major, exact fp32 (MFMA f32).
@@ -275,6 +294,18 @@ vs_status vs_wavelet_filter(int type, int order, float *out);
 vs_status vs_detect_peaks(const float *x, size_t n, int type, int *pos_dev,
                           float *val_dev, size_t capacity,
                           unsigned long long *count_dev, vs_stream_t stream);
+/// Extrema of `rows` signals of n samples (x_stride floats apart) in one
+/// launch sequence, no host synchronisation: results of all rows back to
+/// back in (row, position) order, row r's in
+/// [row_start_dev[r], row_start_dev[r + 1]) (rows + 1 entries; the last is
+/// the total).  Positions are indices inside the row: int32, or int64 when
+/// pos64 != 0 (required for n >= 2^31; the reference's size argument is a
+/// size_t, inc/simd/detect_peaks.h:61-62).  Call with capacity 0 to size the
+/// outputs, then again with the arrays.
+vs_status vs_detect_peaks_batched(const float *x, size_t n, int64_t x_stride, size_t rows,
+                                  int type, void *pos_dev, int pos64, float *val_dev,
+                                  size_t capacity, unsigned long long *row_start_dev,
+                                  vs_stream_t stream);
 
 SIMD_API_END
 

@@ -74,3 +74,59 @@ def test_device_paths_vs_numpy(n, off):
             k = min(cap, len(want))
             assert np.array_equal(pos.cpu().numpy()[:k], want[:k])
             assert np.array_equal(val.cpu().numpy()[:k], xh[want[:k]])
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("rows,n,kind", [(1, 4000, 3), (7, 5000, 1), (33, 4097, 2), (5, 12289, 3)])
+def test_batched_rows_match_single_rows(dev, rows, n, kind):
+    """vs_detect_peaks_batched: every row's segment equals the single-row
+    result (the scalar definition), row_start is the CSR index."""
+    import torch
+    from veles.simd_amd import ops
+    g = torch.Generator().manual_seed(rows * 1000 + n)
+    x = torch.randn(rows, n, generator=g).to(dev)
+    pos, val, rs = ops.detect_peaks_batched(x, kind)
+    assert rs.shape == (rows + 1,) and rs[0] == 0 and rs[-1] == pos.numel()
+    rs = rs.tolist()
+    for r in range(rows):
+        row = x[r].double().cpu()
+        d1 = row[1:-1] - row[:-2]
+        d2 = row[1:-1] - row[2:]
+        m = (d1 * d2 > 0) & (((d1 > 0) & bool(kind & 1)) | ((d1 < 0) & bool(kind & 2)))
+        ref = torch.nonzero(m).flatten() + 1
+        got = pos[rs[r]:rs[r + 1]].cpu().long()
+        assert torch.equal(got, ref), (r, got[:5], ref[:5])
+        assert torch.equal(val[rs[r]:rs[r + 1]].cpu(), x[r].cpu()[ref])
+
+
+@pytest.mark.gpu
+def test_batched_strided_unaligned_rows():
+    """Rows with a stride that is not a multiple of 4 floats and an
+    unaligned base take the scalar kernels."""
+    import torch
+    from veles.simd_amd import ops
+    base = torch.randn(6 * 1003 + 1, device="cuda")
+    x = base[1:].reshape(6, 1003)[:, :1001]          # stride 1003, base offset 4 bytes
+    pos, val, rs = ops.detect_peaks_batched(x, 3)
+    pos_c, val_c, rs_c = ops.detect_peaks_batched(x.cpu(), 3)
+    assert torch.equal(pos.cpu(), pos_c) and torch.equal(rs.cpu(), rs_c)
+    assert torch.equal(val.cpu(), val_c)
+
+
+@pytest.mark.gpu
+def test_matched_filter_batch_in_one_launch_sequence():
+    """MatchedFilter over 4096 x 65536: correlation, batched peak search and
+    thresholding with a single host read, against the per-row path."""
+    import torch
+    from veles.simd_amd import models, ops
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(4096, 65536, device="cuda", generator=g)
+    t = torch.sin(torch.arange(64, device="cuda") * 0.3)
+    mf = models.MatchedFilter(t, threshold=12.0).cuda()
+    resp, peaks = mf(x)
+    assert len(peaks) == 4096
+    for r in (0, 1, 2047, 4095):
+        p, v = ops.detect_peaks(resp[r], ops.signal.MAXIMUM)
+        keep = v > 12.0
+        assert torch.equal(peaks[r][0], p[keep]) and torch.equal(peaks[r][1], v[keep])
+    assert sum(p.numel() for p, _ in peaks) > 0

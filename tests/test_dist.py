@@ -107,6 +107,26 @@ def test_sgemm_rowsplit(world):
 
 
 @pytest.mark.gpu
+def test_sgemm_rowsplit_device_fewer_rows_than_ranks():
+    """m < ranks: the ranks that own no rows pass an empty A (data_ptr 0)."""
+    import torch
+    world, batch, m, k, n = 4, 2, 3, 20, 17
+    g = torch.Generator(device="cuda").manual_seed(0)
+    a = torch.randn(batch, m, k, device="cuda", generator=g)
+    b = torch.randn(batch, k, n, device="cuda", generator=g)
+    ref = (a.double() @ b.double()).float()
+    with _group(world) as grp:
+        rows = [native.shard(m, world, r) for r in range(world)]
+        assert any(rc == 0 for _, rc in rows)
+        a_rows = [a[:, r0:r0 + rc].contiguous() for r0, rc in rows]
+        bs = [b.clone() for _ in range(world)]
+        cs = [torch.full((batch, m, n), float("nan"), device="cuda") for _ in range(world)]
+        grp.sgemm_rowsplit_device(a_rows, bs, cs)
+    for c in cs:
+        torch.testing.assert_close(c, ref, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", WORLDS)
 def test_sgemm_rowsplit_device(world):
     """Device-resident row split: every rank's C holds the whole product

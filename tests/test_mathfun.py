@@ -117,3 +117,26 @@ def test_math_ops_device_api():
     got = ops.pow(xp, y).cpu().numpy()
     want = torch.pow(xp.double(), y.double()).float().cpu().numpy()
     assert (_ulps(got, want) <= 4).all()
+
+
+@pytest.mark.gpu
+def test_device_math_header_composes():
+    """<simd/device_math.h> from a kernel that includes nothing else of the
+    library (csrc/kernels/device_math_user.hip): a Morlet atom and a log-power
+    feature against float64."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    t = torch.linspace(-6, 6, 100001, device="cuda")
+    mor = torch.empty_like(t)
+    feat = torch.empty_like(t)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.call("vs_device_math_example", t.data_ptr(), 5.0, 1.5, t.numel(), mor.data_ptr(),
+              feat.data_ptr(), s)
+    td = t.double()
+    ref_m = torch.exp(-0.5 * td * td) * torch.cos(5.0 * td)
+    ref_f = torch.log(1 + torch.sqrt(td.abs() ** 1.5))
+    # cos(5 t) carries the float rounding of 5 t (|5 t| <= 30: 2e-6 absolute)
+    assert (mor.double() - ref_m).abs().max().item() < 4e-6
+    # 1 + sqrt(.) is rounded to float before the log: 6e-8 absolute
+    assert (feat.double() - ref_f).abs().max().item() < 5e-7

@@ -107,3 +107,37 @@ def test_normalize2d_device_strided(h, w, sstride, dstride, off):
     torch.testing.assert_close(got[:, :w], want, atol=0, rtol=0)
     if dstride > w:
         assert (got[:, w:] == 7.0).all()
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_batched_planes(dev):
+    """A stack of planes in one launch: each plane normalised with its own
+    min / max (one flat plane gives zeros), equal to the per-plane op."""
+    import torch
+    from veles.simd_amd import ops
+    g = torch.Generator().manual_seed(4)
+    img = torch.randint(0, 256, (5, 3, 37, 53), dtype=torch.uint8, generator=g)
+    img[1, 2] = 77                                   # flat plane
+    img[0, 0] = img[0, 0] // 4 + 100                 # narrow range
+    x = img.to(dev)
+    out = ops.normalize2d(x)
+    mm = ops.minmax(x)
+    assert out.shape == x.shape and mm.shape == (5, 3, 2)
+    for i in range(5):
+        for j in range(3):
+            ref = ops.normalize2d(x[i, j])
+            assert torch.equal(out[i, j], ref)
+            assert mm[i, j, 0] == x[i, j].min() and mm[i, j, 1] == x[i, j].max()
+    assert (out[1, 2] == 0).all()
+
+
+@pytest.mark.gpu
+def test_batched_planes_strided():
+    """Planes cut out of a larger tensor (row stride > width, plane stride > plane)."""
+    import torch
+    from veles.simd_amd import ops
+    big = torch.randint(0, 256, (4, 40, 64), dtype=torch.uint8, device="cuda")
+    x = big[:, 3:35, 5:50]
+    out = ops.normalize2d(x)
+    for i in range(4):
+        assert torch.equal(out[i], ops.normalize2d(x[i].contiguous()))

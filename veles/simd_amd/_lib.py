@@ -55,6 +55,10 @@ _SIGNATURES = {
     "vs_sum": (_i, [_vp, _sz, _vp, _vp]),
     "vs_minmax": (_i, [_vp, _sz, _vp, _vp]),
     "vs_minmax2d_u8": (_i, [_vp, _i, _i, _i, _vp, _vp]),
+    "vs_minmax2d_u8_batched": (_i, [_vp, _i, _i64, _i, _i, _i, _vp, _vp]),
+    "vs_normalize2d_u8_batched": (_i, [_vp, _i, _i64, _i, _i, _i, _vp, _i, _i, _vp, _i, _i64,
+                                       _vp]),
+    "vs_detect_peaks_batched": (_i, [_vp, _sz, _i64, _sz, _i, _vp, _i, _vp, _sz, _vp, _vp]),
     "vs_normalize2d_u8": (_i, [_vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
     "vs_sgemm": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _vp, _i64, _f, _vp,
                       _i64, _vp]),
@@ -70,6 +74,7 @@ _SIGNATURES = {
     "vs_sgemm_bf16x3_strided_batched": (_i, [_i, _i, _i, _i, _i, _f, _vp, _i64, _i64,
                                              _vp, _i64, _i64, _f, _vp, _i64, _i64, _i,
                                              _vp]),
+    "vs_device_math_example": (_i, [_vp, _f, _f, ctypes.c_size_t, _vp, _vp, _vp]),
     "vs_sgemm_variant": (_i, [_i, _i, _i, _i, _i, _i, _f, _vp, _i64, _vp, _i64, _f,
                               _vp, _i64, _vp]),
     "vs_sgemm_variant_batched": (_i, [_i, _i, _i, _i, _i, _i, _f, _vp, _i64, _i64, _vp, _i64,

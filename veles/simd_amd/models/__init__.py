@@ -18,10 +18,13 @@ def _cached_plan(mod: nn.Module, taps: torch.Tensor, x: torch.Tensor, algorithm,
                  correlate: bool):
     """Inference with fixed taps on the GPU: a Conv1dPlan (filter spectra
     computed once) cached on `mod`, keyed by signal length, device and the
-    taps' storage and version counter; None when autograd or the CPU path
-    applies."""
-    if (not x.is_cuda or x.dtype != torch.float32 or taps.requires_grad
-            and torch.is_grad_enabled()):
+    taps' storage and version counter; None on the CPU path, for trainable
+    taps (their version changes every step) and while torch.compile traces
+    (plan creation reads data pointers, which fake tensors do not have).
+    The plan is run through Conv1dPlan.apply, a custom op with a backward,
+    so gradients still reach x."""
+    if (not x.is_cuda or x.dtype != torch.float32 or torch.compiler.is_compiling()
+            or taps.requires_grad and torch.is_grad_enabled()):
         return None
     key = (x.shape[-1], x.device, taps._version, taps.data_ptr(), correlate)
     if getattr(mod, "_plan_key", None) != key:
@@ -54,7 +57,8 @@ class FIRFilter(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         plan = self._planned(x)
-        y = plan(x) if plan is not None else ops.conv1d(x, self.taps, self.algorithm)
+        y = (plan.apply(x, self.taps) if plan is not None
+             else ops.conv1d(x, self.taps, self.algorithm))
         H = self.taps.shape[-1]
         X = x.shape[-1]
         if self.mode == "same":
@@ -76,12 +80,15 @@ class MatchedFilter(nn.Module):
 
     def forward(self, x: torch.Tensor):
         plan = _cached_plan(self, self.template, x, "auto", True)
-        resp = plan(x) if plan is not None else ops.correlate(x, self.template)
-        out = []
-        for row in resp.reshape(-1, resp.shape[-1]):
-            pos, val = ops.detect_peaks(row, ops.signal.MAXIMUM)
-            keep = val > self.threshold
-            out.append((pos[keep], val[keep]))
+        resp = (plan.apply(x, self.template) if plan is not None
+                else ops.correlate(x, self.template))
+        # all rows in one launch sequence; one host read (the per-row counts)
+        pos, val, row_start = ops.detect_peaks_batched(resp.detach(), ops.signal.MAXIMUM)
+        keep = val > self.threshold
+        kept = torch.cat([keep.new_zeros(1, dtype=torch.int64), keep.cumsum(0)])
+        bounds = kept[row_start].tolist()
+        pos, val = pos[keep], val[keep]
+        out = [(pos[a:b], val[a:b]) for a, b in zip(bounds[:-1], bounds[1:])]
         return resp, out
 
 
@@ -139,10 +146,7 @@ class ImageNormalizer(nn.Module):
     """uint8 planes -> float32 in [-1, 1] (normalize.h normalize2D)."""
 
     def forward(self, img: torch.Tensor) -> torch.Tensor:
-        if img.dim() == 2:
-            return ops.normalize2d(img)
-        return torch.stack([ops.normalize2d(p) for p in img.reshape(-1, *img.shape[-2:])]
-                           ).reshape(*img.shape)
+        return ops.normalize2d(img)   # every plane of the stack in one launch
 
 
 class Linear(nn.Module):

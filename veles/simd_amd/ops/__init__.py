@@ -12,7 +12,7 @@ from .elementwise import (add, affine, binary, complex_conjugate,  # noqa: F401
                           minmax, mul, normalize2d, pow, saxpy, sin, sincos, sqrt, sub,
                           sum_all)
 from .signal import (Conv1dPlan, conv1d, conv1d_algorithm, correlate, detect_peaks,  # noqa: F401
-                     dwt, fft, irfft, rfft, swt, swt_level, wavedec,
+                     detect_peaks_batched, dwt, fft, irfft, rfft, swt, swt_level, wavedec,
                      wavelet_filter)
 
 __all__ = [
@@ -20,5 +20,5 @@ __all__ = [
     "mul", "complex_multiply", "complex_conjugate", "affine", "saxpy", "math",
     "sin", "cos", "log", "exp", "sum_all", "minmax", "normalize2d", "conv1d",
     "correlate", "conv1d_algorithm", "Conv1dPlan", "fft", "rfft", "irfft", "dwt", "swt",
-    "wavedec", "wavelet_filter", "detect_peaks", "swt_level",
+    "wavedec", "wavelet_filter", "detect_peaks", "detect_peaks_batched", "swt_level",
 ]

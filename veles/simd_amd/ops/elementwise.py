@@ -266,20 +266,26 @@ def _(x):
 
 @torch.library.custom_op("veles::minmax", mutates_args=())
 def minmax(x: torch.Tensor) -> torch.Tensor:
-    """[min, max] of a float32 tensor (minmax1D) or a uint8 2-D plane
-    (minmax2D)."""
+    """[min, max] of a float32 tensor (minmax1D), or of a uint8 plane
+    (minmax2D) -- for a stack of planes [..., h, w] one pair per plane,
+    shape [..., 2], all planes in one launch sequence."""
     if x.dtype == torch.uint8:
-        if x.dim() != 2:
-            raise ValueError("veles::minmax: uint8 input must be 2-D")
+        if x.dim() < 2:
+            raise ValueError("veles::minmax: uint8 input must be [..., h, w]")
+        lead = x.shape[:-2]
         if not _gpu(x, "veles::minmax"):
-            return torch.stack([x.min(), x.max()])
-        out = torch.empty(2, dtype=torch.uint8, device=x.device)
-        if x.stride(1) != 1:
-            x = x.contiguous()
+            flat = x.reshape(*lead, -1)
+            return torch.stack([flat.min(-1).values, flat.max(-1).values], -1)
+        h, w = x.shape[-2:]
+        xp = x.reshape(-1, h, w)
+        if xp.stride(2) != 1 or (xp.shape[0] > 1 and xp.stride(0) < (h - 1) * xp.stride(1) + w):
+            xp = xp.contiguous()
+        planes = xp.shape[0]
+        out = torch.empty((planes, 2), dtype=torch.uint8, device=x.device)
         with on_device(x):
-            _lib.call("vs_minmax2d_u8", ptr(x), x.stride(0), x.shape[1],
-                      x.shape[0], ptr(out), stream_of(x))
-        return out
+            _lib.call("vs_minmax2d_u8_batched", ptr(xp), xp.stride(1), xp.stride(0), w, h,
+                      planes, ptr(out), stream_of(x))
+        return out.reshape(*lead, 2)
     if not _gpu(x, "veles::minmax"):
         return torch.stack([x.min(), x.max()])
     x = x.contiguous()
@@ -291,31 +297,40 @@ def minmax(x: torch.Tensor) -> torch.Tensor:
 
 @minmax.register_fake
 def _(x):
+    if x.dtype == torch.uint8:
+        return x.new_empty((*x.shape[:-2], 2))
     return x.new_empty((2,))
 
 
 @torch.library.custom_op("veles::normalize2d", mutates_args=())
 def normalize2d(x: torch.Tensor) -> torch.Tensor:
-    """uint8 plane -> float32 in [-1, 1] (normalize2D), min/max found and
-    applied on the device without a host round trip."""
-    if x.dtype != torch.uint8 or x.dim() != 2:
-        raise ValueError("veles::normalize2d expects a 2-D uint8 tensor")
+    """uint8 plane(s) [..., h, w] -> float32 in [-1, 1] (normalize2D), each
+    plane with its own min / max, found and applied on the device without a
+    host round trip; a stack of planes takes one launch sequence."""
+    if x.dtype != torch.uint8 or x.dim() < 2:
+        raise ValueError("veles::normalize2d expects a uint8 tensor [..., h, w]")
+    h, w = x.shape[-2:]
     if not _gpu(x, "veles::normalize2d"):
-        mn, mx = int(x.min()), int(x.max())
-        if mn == mx:
-            return torch.zeros(x.shape, dtype=torch.float32)
-        return (x.float() - mn) / ((mx - mn) / 2.0) - 1.0
-    if x.stride(1) != 1:
-        x = x.contiguous()
-    h, w = x.shape
-    out = torch.empty((h, w), dtype=torch.float32, device=x.device)
-    mm = torch.empty(2, dtype=torch.uint8, device=x.device)
+        flat = x.reshape(-1, h * w).float()
+        mn = flat.min(-1, keepdim=True).values
+        mx = flat.max(-1, keepdim=True).values
+        span = (mx - mn) / 2.0
+        res = torch.where(span > 0, (flat - mn) / span.clamp_min(1e-30) - 1.0,
+                          torch.zeros_like(flat))
+        return res.reshape(x.shape)
+    xp = x.reshape(-1, h, w)
+    if xp.stride(2) != 1 or (xp.shape[0] > 1 and xp.stride(0) < (h - 1) * xp.stride(1) + w):
+        xp = xp.contiguous()
+    planes = xp.shape[0]
+    out = torch.empty((planes, h, w), dtype=torch.float32, device=x.device)
+    mm = torch.empty((planes, 2), dtype=torch.uint8, device=x.device)
     with on_device(x):
         s = stream_of(x)
-        _lib.call("vs_minmax2d_u8", ptr(x), x.stride(0), w, h, ptr(mm), s)
-        _lib.call("vs_normalize2d_u8", ptr(x), x.stride(0), w, h, ptr(mm), 0, 0,
-                  ptr(out), w, s)
-    return out
+        _lib.call("vs_minmax2d_u8_batched", ptr(xp), xp.stride(1), xp.stride(0), w, h, planes,
+                  ptr(mm), s)
+        _lib.call("vs_normalize2d_u8_batched", ptr(xp), xp.stride(1), xp.stride(0), w, h,
+                  planes, ptr(mm), 0, 0, ptr(out), w, h * w, s)
+    return out.reshape(x.shape)
 
 
 @normalize2d.register_fake

@@ -8,6 +8,7 @@ CPU tensors run an fp64-accumulated torch reference of the same math.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
@@ -94,6 +95,13 @@ class Conv1dPlan:
         self.algorithm = {v: k for k, v in ALGORITHMS.items()}.get(algo.value, algo.value)
         self.precomputed = bool(pre.value)
         self._stream_used = torch.cuda.current_stream(h.device)
+        _PLANS[id(self)] = self
+
+    def apply(self, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+        """Differentiable, torch.compile-traceable execution: the plan runs
+        the forward; gradients to x and to h (the taps the plan was built
+        from) come from the conv1d op's backward."""
+        return _conv1d_planned(x, h, id(self), _algo(self.algorithm), self.correlate)
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if x.shape[-1] != self.x_len or x.dtype != torch.float32 or x.device != self.device:
@@ -119,8 +127,28 @@ class Conv1dPlan:
             self._plan = ctypes.c_void_p()
 
 
+# Live plans by id(): the planned op takes the id (custom-op schemas have no
+# object arguments) and falls back to the plain op when the plan is gone.
+_PLANS: "weakref.WeakValueDictionary[int, Conv1dPlan]" = weakref.WeakValueDictionary()
+
+
+@torch.library.custom_op("veles::conv1d_planned", mutates_args=())
+def _conv1d_planned(x: torch.Tensor, h: torch.Tensor, plan_id: int, algorithm: int,
+                    correlate: bool) -> torch.Tensor:
+    plan = _PLANS.get(plan_id)
+    if (plan is None or not x.is_cuda or x.dtype != torch.float32
+            or x.shape[-1] != plan.x_len or x.device != plan.device):
+        return _conv1d(x, h, algorithm, correlate)
+    return plan(x)
+
+
+@_conv1d_planned.register_fake
+def _(x, h, plan_id, algorithm, correlate):
+    return x.new_empty((*x.shape[:-1], x.shape[-1] + h.shape[-1] - 1))
+
+
 def _conv_setup(ctx, inputs, output):
-    x, h, algorithm, corr = inputs
+    x, h, algorithm, corr = inputs[0], inputs[1], inputs[-2], inputs[-1]
     ctx.save_for_backward(x, h)
     ctx.algorithm = algorithm
     ctx.corr = corr
@@ -146,6 +174,8 @@ def _conv_backward(ctx, g):
 
 
 _conv1d.register_autograd(_conv_backward, setup_context=_conv_setup)
+_conv1d_planned.register_autograd(lambda ctx, g: _conv_backward(ctx, g)[:2] + (None, None, None),
+                                  setup_context=_conv_setup)
 
 
 def conv1d(x: torch.Tensor, h: torch.Tensor, algorithm="auto",
@@ -414,28 +444,69 @@ def wavedec(x, family="daubechies", order=8, levels=1, ext="periodic"):
 MAXIMUM, MINIMUM, BOTH = 1, 2, 3
 
 
-def detect_peaks(x: torch.Tensor, kind=BOTH):
-    """Strict extrema of a 1-D float32 tensor: (positions int32, values)."""
-    kind = {"max": 1, "min": 2, "both": 3}.get(kind, kind)
-    if not x.is_cuda:
-        xd = x.float()
-        d1 = xd[1:-1] - xd[:-2]
-        d2 = xd[1:-1] - xd[2:]
+def _peaks_host(xr: torch.Tensor, kind: int, pos_dtype):
+    """Scalar definition (src/detect_peaks.c:123-125) row by row."""
+    pos, val, starts = [], [], [0]
+    for row in xr.float():
+        d1 = row[1:-1] - row[:-2]
+        d2 = row[1:-1] - row[2:]
         m = (d1 * d2) > 0
         m &= ((d1 > 0) & bool(kind & 1)) | ((d1 < 0) & bool(kind & 2))
-        pos = torch.nonzero(m).flatten().int() + 1
-        return pos, xd[pos.long()]
+        p = torch.nonzero(m).flatten() + 1
+        pos.append(p.to(pos_dtype))
+        val.append(row[p])
+        starts.append(starts[-1] + p.numel())
+    return torch.cat(pos), torch.cat(val), torch.tensor(starts, dtype=torch.int64)
+
+
+@torch.library.custom_op("veles::detect_peaks", mutates_args=())
+def _detect_peaks(x: torch.Tensor, kind: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Strict extrema of every row of x [rows, n] (float32): positions inside
+    the row (int32; int64 for n >= 2^31), values, and row_start [rows + 1]
+    (row r's results are [row_start[r], row_start[r + 1])).  One launch
+    sequence and one host read (the total) for all rows."""
+    if x.dim() != 2 or x.dtype != torch.float32:
+        raise ValueError("veles::detect_peaks expects a float32 [rows, n] tensor")
+    rows, n = x.shape
+    pos_dtype = torch.int64 if n >= (1 << 31) else torch.int32
+    if not x.is_cuda:
+        return _peaks_host(x, kind, pos_dtype)
     require_gpu_tensor(x, "veles::detect_peaks")
-    xc = x.contiguous()
-    n = xc.numel()
-    cnt = torch.zeros(1, dtype=torch.int64, device=x.device)
+    xc = x if x.stride(1) == 1 and (rows == 1 or x.stride(0) >= n) else x.contiguous()
+    row_start = torch.empty(rows + 1, dtype=torch.int64, device=x.device)
+    p64 = int(pos_dtype == torch.int64)
     with on_device(x):
         s = stream_of(x)
-        _lib.call("vs_detect_peaks", ptr(xc), n, kind, None, None, 0, ptr(cnt), s)
-        total = int(cnt.item())
-        pos = torch.empty(total, dtype=torch.int32, device=x.device)
+        _lib.call("vs_detect_peaks_batched", ptr(xc), n, xc.stride(0), rows, kind, None, p64,
+                  None, 0, ptr(row_start), s)
+        total = int(row_start[-1].item())
+        pos = torch.empty(total, dtype=pos_dtype, device=x.device)
         val = torch.empty(total, dtype=torch.float32, device=x.device)
         if total:
-            _lib.call("vs_detect_peaks", ptr(xc), n, kind, ptr(pos), ptr(val), total,
-                      ptr(cnt), s)
+            _lib.call("vs_detect_peaks_batched", ptr(xc), n, xc.stride(0), rows, kind, ptr(pos),
+                      p64, ptr(val), total, ptr(row_start), s)
+    return pos, val, row_start
+
+
+@_detect_peaks.register_fake
+def _(x, kind):
+    nnz = torch.library.get_ctx().new_dynamic_size()
+    pos_dtype = torch.int64 if x.shape[1] >= (1 << 31) else torch.int32
+    return (x.new_empty(nnz, dtype=pos_dtype), x.new_empty(nnz),
+            x.new_empty(x.shape[0] + 1, dtype=torch.int64))
+
+
+def _kind(kind) -> int:
+    return {"max": 1, "min": 2, "both": 3}.get(kind, kind)
+
+
+def detect_peaks(x: torch.Tensor, kind=BOTH):
+    """Strict extrema of a 1-D float32 tensor: (positions, values)."""
+    pos, val, _ = _detect_peaks(x.reshape(1, -1), _kind(kind))
     return pos, val
+
+
+def detect_peaks_batched(x: torch.Tensor, kind=BOTH):
+    """Strict extrema of every row of x [..., n]: (positions, values,
+    row_start); row r's results are [row_start[r], row_start[r + 1])."""
+    return _detect_peaks(x.reshape(-1, x.shape[-1]), _kind(kind))

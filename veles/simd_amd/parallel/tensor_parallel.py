@@ -28,6 +28,19 @@ def _sgemm_into(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> None:
         return
     m, k = a.shape
     n = b.shape[1]
+    # vs_sgemm reads and writes raw pointers: everything it assumes is
+    # checked here (a wrong dtype or shape would read or write past the tensors)
+    for name, t in (("a", a), ("b", b), ("c", c)):
+        if t.dtype != torch.float32 or t.device != a.device:
+            raise TypeError(f"rowsplit_bmm: {name} must be float32 on {a.device}, "
+                            f"got {t.dtype} on {t.device}")
+    if b.dim() != 2 or b.shape[0] != k:
+        raise ValueError(f"rowsplit_bmm: b has shape {tuple(b.shape)}, expected ({k}, n)")
+    if tuple(c.shape) != (m, n) or not c.is_contiguous():
+        raise ValueError(f"rowsplit_bmm: out block must be contiguous ({m}, {n}), "
+                         f"got {tuple(c.shape)} contiguous={c.is_contiguous()}")
+    if not (a.is_contiguous() and b.is_contiguous()):
+        raise ValueError("rowsplit_bmm: operands must be contiguous")
     with on_device(a):
         _lib.call("vs_sgemm", 0, 0, m, n, k, 1.0, ptr(a), k, ptr(b), n, 0.0, ptr(c), n,
                   stream_of(a))
