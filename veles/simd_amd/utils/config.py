@@ -37,8 +37,12 @@ KNOBS = [
          "csrc/runtime/runtime.cpp"),
     Knob("VELES_ZERO_COPY", "1", "0: stage every small host operand into device memory "
          "instead of the mapped pinned arena", "csrc/runtime/runtime.cpp"),
-    Knob("VELES_SGEMM_VARIANT", "-1", "force an SGEMM kernel variant "
-         "(0..VS_SGEMM_VARIANTS-1, include/simd/gpu.h) for tuning", "csrc/kernels/sgemm.hip"),
+    Knob("VELES_SGEMM_VARIANT", "-1", "force an SGEMM tile (0 / 1 / 2: 64 / 128 / 256 tiles "
+         "with automatic k slicing, 3..5: whole tiles only; include/simd/gpu.h) for tuning",
+         "csrc/kernels/sgemm.hip"),
+    Knob("VELES_SCRATCH_CACHE_MB", "8192", "cap of the device scratch cache (freed blocks "
+         "kept for reuse, per stream); above it the oldest blocks are released",
+         "csrc/runtime/runtime.cpp"),
     Knob("VELES_GEMM_BF16_VARIANT", "-1", "force a bf16 GEMM variant (0: 128 tiles, "
          "1: large tiles)", "csrc/kernels/gemm_bf16.hip"),
     Knob("VELES_GEMM_BF16_PACK", "-1", "force (1) or forbid (0) the bf16 operand pre-pack "
