@@ -8,9 +8,10 @@ aggregate GFLOP/s (weak scaling: every rank multiplies its own pair of
 matrices).  The second half of the metric, 1D convolution throughput at
 signal length 2^20 (filter 4096, batch 64 per GPU, auto-selected algorithm),
 is timed the same way and reported in `secondary`, as are two
-communication-bearing BASELINE configurations: row-split batched SGEMM
-8192^2 (C row blocks all-gathered over RCCL / xGMI, config 5) and the SWT
-db8 x 8 levels over 65536 signals sharded data-parallel (config 4).
+other BASELINE configurations: overlap-save convolution 2^22 x 4096 taps,
+batch 256 (config 3), row-split batched SGEMM 8192^2 x 64 (C row blocks
+all-gathered over RCCL / xGMI, config 5) and the SWT db8 x 8 levels over
+65536 signals sharded data-parallel (config 4).
 
 Run: python bench.py --gpus N --steps K --warmup W   (N > 1 under
 torch.distributed.run; one rank per GPU, RCCL backend).
@@ -203,6 +204,39 @@ def main():
             lib.vs_conv1d_plan_destroy(plan)
             secondary["conv1d_plan_msamples_per_s"] = round(
                 CONV_LEN * CONV_BATCH * csteps * world / dtp / 1e6, 1)
+        del x, y
+        # BASELINE config 3: overlap-save convolution, signal 2^22, filter
+        # 4096, batch 256 (per GPU), per call and through a plan
+        c3_len, c3_batch = 1 << 22, 256
+        x3 = torch.randn((c3_batch, c3_len), device="cuda", generator=g)
+        y3len = c3_len + CONV_H - 1
+        y3 = torch.empty((c3_batch, y3len), device="cuda")
+        px3, py3 = (ctypes.c_void_p(t.data_ptr()) for t in (x3, y3))
+
+        def conv3_step():
+            st = lib.vs_conv1d(3, 0, px3, c3_len, c3_len, ph, CONV_H, 0, py3, y3len, c3_batch,
+                               stream)
+            if st:
+                raise RuntimeError(lib.vs_last_error().decode())
+
+        c3steps = max(10, args.steps // 2)
+        dt3c = _timed(conv3_step, c3steps, 2, dist_on)
+        secondary["conv1d_os_2^22x4096x256_msamples_per_s"] = round(
+            c3_len * c3_batch * c3steps * world / dt3c / 1e6, 1)
+        secondary["conv1d_os_2^22x4096x256_ms_per_step"] = round(dt3c / c3steps * 1e3, 3)
+        plan3 = ctypes.c_void_p()
+        if lib.vs_conv1d_plan_create(3, 0, c3_len, ph, CONV_H, 0, 1, ctypes.byref(plan3),
+                                     stream) == 0:
+            def plan3_step():
+                st = lib.vs_conv1d_plan_execute(plan3, px3, c3_len, py3, y3len, c3_batch, stream)
+                if st:
+                    raise RuntimeError(lib.vs_last_error().decode())
+            dt3p = _timed(plan3_step, c3steps, 2, dist_on)
+            torch.cuda.synchronize()
+            lib.vs_conv1d_plan_destroy(plan3)
+            secondary["conv1d_os_2^22x4096x256_plan_msamples_per_s"] = round(
+                c3_len * c3_batch * c3steps * world / dt3p / 1e6, 1)
+        del x3, y3
         secondary.update({
             "conv1d_msamples_per_s": round(msamples, 1),
             "conv1d_ms_per_step": round(dtc / csteps * 1e3, 3),
@@ -213,21 +247,22 @@ def main():
         })
 
     # ------------------------------------- comm-bearing BASELINE configs
-    # Config 5 (row-split batched SGEMM 8192^2, RCCL all-gather of the C row
-    # blocks over xGMI, overlapped with the next matrix's GEMM; batch 8 of
-    # the config's 64 to stay within the bench's time budget) and config 4
+    # Config 5 (row-split batched SGEMM 8192^2 x 64, RCCL all-gather of the C
+    # row blocks over xGMI, overlapped with the next matrix's GEMM: every rank
+    # holds its rows of the 64 A matrices, all of B and the gathered C,
+    # 34-48 GiB per GPU) and config 4
     # (SWT db8 x 8 levels over 65536 x 1024 signals, batch sharded over the
     # ranks).  Both run under the same barrier / max-over-ranks clock.
     if not args.no_comm:
         from veles.simd_amd import parallel
-        rs_n, rs_batch = 8192, 8
+        rs_n, rs_batch = 8192, 64
         m_loc = rs_n // world
         ga = torch.Generator(device="cuda").manual_seed(77 + rank)
         a_loc = torch.rand(rs_batch, m_loc, rs_n, device="cuda", generator=ga) - 0.5
         bmat = torch.rand(rs_batch, rs_n, rs_n, device="cuda",
                           generator=torch.Generator(device="cuda").manual_seed(99)) - 0.5
         cfull = torch.empty(rs_batch, m_loc * world, rs_n, device="cuda")
-        rsteps = max(2, args.steps // 10)
+        rsteps = max(2, args.steps // 20)
         dtr = _timed(lambda: parallel.rowsplit_bmm(a_loc, bmat, out=cfull), rsteps, 1, dist_on)
         # numerics: this rank's rows of the first matrix, 64 rows
         r0 = rank * m_loc
@@ -239,6 +274,7 @@ def main():
         secondary.update({
             "rowsplit_sgemm_gflops": round(2.0 * rs_n ** 3 * rs_batch * rsteps / dtr / 1e9, 1),
             "rowsplit_ms_per_step": round(dtr / rsteps * 1e3, 2),
+            "rowsplit_ms_per_matrix": round(dtr / rsteps / rs_batch * 1e3, 3),
             "rowsplit_allgather_GB_per_rank_per_step": round(
                 rs_batch * (world - 1) * m_loc * rs_n * 4 / 1e9, 3),
             "rowsplit_config": {"n": rs_n, "batch": rs_batch, "parallelism": f"tp{world}",

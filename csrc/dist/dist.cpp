@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -325,6 +326,54 @@ struct RankBuffers {
   }
 };
 
+// Events of one rank's call, destroyed with the list.
+struct EventList {
+  std::vector<hipEvent_t> ev;
+  ~EventList() {
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+  vs_status record(hipStream_t s) {
+    hipEvent_t e = nullptr;
+    VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev.push_back(e);
+    VS_HIP(hipEventRecord(e, s));
+    return VS_OK;
+  }
+};
+
+// f(r) for every rank, each on a host thread of its own bound to the rank's
+// device.  The sharded entry points take pageable host arrays, and a copy
+// from or to pageable memory blocks the issuing thread until it is done: in
+// one thread, rank r + 1's work would not even be enqueued before rank r's
+// download has finished.  With one thread per rank every rank's copies and
+// kernels are issued at once and the devices (and PCIe links) run side by
+// side.  Collectives stay on the calling thread, between such phases.
+template <class F>
+vs_status for_ranks(vs_dist_context *c, F &&f) {
+  if (c->n == 1) {
+    DevGuard g(c->dev[0]);
+    return f(0);
+  }
+  std::vector<vs_status> st(c->n, VS_OK);
+  std::vector<std::string> err(c->n);
+  std::vector<std::thread> th;
+  th.reserve(c->n);
+  for (int r = 0; r < c->n; r++)
+    th.emplace_back([&, r] {
+      DevGuard g(c->dev[r]);
+      st[r] = f(r);
+      if (st[r] != VS_OK) err[r] = last_error();
+    });
+  for (auto &t : th) t.join();
+  for (int r = 0; r < c->n; r++)
+    if (st[r] != VS_OK) {
+      set_error("rank %d: %s", r, err[r].c_str());
+      return st[r];
+    }
+  return VS_OK;
+}
+
 vs_status check_ctx(vs_dist_context *c) {
   VS_REQUIRE(c, "vs_dist: null context");
   VS_REQUIRE(!c->aborted, "vs_dist: communicator was aborted after an error");
@@ -531,44 +580,42 @@ vs_status vs_dist_sgemm_rowsplit(vs_dist_t c, int m, int n, int k, const float *
   VS_TRY(dA.alloc(c, abytes));
   VS_TRY(dB.alloc(c, batch * kn * sizeof(float)));
   VS_TRY(dC.alloc(c, cbytes));
-  for (int r = 0; r < R; r++)
+  // uploads: every rank's rows of A from its own host thread; B crosses
+  // PCIe once (to rank 0) and reaches the other ranks over xGMI
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
     for (int b = 0; b < batch; b++)
       VS_TRY(h2d(c->dev[r], dA.f(r) + b * rc[r] * k,
                  A + (static_cast<size_t>(b) * m + rb[r]) * k, rc[r] * k * sizeof(float),
                  c->main[r]));
-  // B crosses PCIe once (to rank 0) and reaches the other ranks over xGMI
-  VS_TRY(h2d(c->dev[0], dB.f(0), B, batch * kn * sizeof(float), c->main[0]));
+    if (r == 0) VS_TRY(h2d(c->dev[0], dB.f(0), B, batch * kn * sizeof(float), c->main[0]));
+    return VS_OK;
+  }));
   {
     auto p = dB.ptrs();
     VS_TRY(broadcast_on(c, c->main, p.data(), batch * kn * sizeof(float), 0));
   }
-  // per matrix: the rank's rows on its main stream, then straight to the
-  // caller's C on the side stream (overlapping the next matrix's GEMM); the
-  // host receives every row block from the rank that computed it, so no
-  // device needs the whole C and nothing is gathered
-  std::vector<hipEvent_t> evs;
-  struct EvFree {
-    std::vector<hipEvent_t> *e;
-    ~EvFree() {
-      for (auto x : *e)
-        if (x) (void)hipEventDestroy(x);
-    }
-  } evfree{&evs};
-  for (int b = 0; b < batch; b++)
-    for (int r = 0; r < R; r++) {
-      if (rc[r] == 0) continue;
-      DevGuard g(c->dev[r]);
-      float *cb = dC.f(r) + b * rc[r] * n;
+  // per rank: every matrix's GEMM is enqueued on the main stream first (each
+  // followed by an event), then the row blocks go straight to the caller's C
+  // on the side stream, block b as soon as GEMM b has finished -- so the
+  // download of matrix b overlaps GEMM b + 1, and the ranks' host threads
+  // never wait for each other.  The host receives every row block from the
+  // rank that computed it: no device needs the whole C, nothing is gathered.
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    if (rc[r] == 0) return VS_OK;
+    EventList evs;
+    for (int b = 0; b < batch; b++) {
       VS_TRY(vs_sgemm(0, 0, static_cast<int>(rc[r]), n, k, 1.f, dA.f(r) + b * rc[r] * k, k,
-                      dB.f(r) + b * kn, n, 0.f, cb, n, c->main[r]));
-      hipEvent_t ev = nullptr;
-      VS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      evs.push_back(ev);
-      VS_HIP(hipEventRecord(ev, c->main[r]));
-      VS_HIP(hipStreamWaitEvent(c->side[r], ev, 0));
-      VS_TRY(d2h(c->dev[r], C + (static_cast<size_t>(b) * m + rb[r]) * n, cb,
-                 rc[r] * n * sizeof(float), c->side[r]));
+                      dB.f(r) + b * kn, n, 0.f, dC.f(r) + b * rc[r] * n, n, c->main[r]));
+      VS_TRY(evs.record(c->main[r]));
     }
+    for (int b = 0; b < batch; b++) {
+      VS_HIP(hipStreamWaitEvent(c->side[r], evs.ev[b], 0));
+      VS_TRY(d2h(c->dev[r], C + (static_cast<size_t>(b) * m + rb[r]) * n,
+                 dC.f(r) + b * rc[r] * n, rc[r] * n * sizeof(float), c->side[r]));
+    }
+    VS_HIP(hipStreamSynchronize(c->side[r]));  // evs may go
+    return VS_OK;
+  }));
   return vs_dist_synchronize(c);
 }
 
@@ -647,16 +694,120 @@ vs_status vs_dist_conv1d_batch(vs_dist_t c, int correlate, const float *x, int x
   VS_TRY(dx.alloc(c, xb));
   VS_TRY(dy.alloc(c, yb));
   VS_TRY(dh.alloc(c, h_len * sizeof(float)));
-  for (int r = 0; r < R; r++) {
-    if (bc[r] == 0) continue;
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    if (bc[r] == 0) return VS_OK;
     VS_TRY(h2d(c->dev[r], dx.f(r), x + bb[r] * x_len, xb[r], c->main[r]));
     VS_TRY(h2d(c->dev[r], dh.f(r), h, h_len * sizeof(float), c->main[r]));
-    DevGuard g(c->dev[r]);
     VS_TRY(vs_conv1d(VS_CONV_AUTO, correlate, dx.f(r), x_len, x_len, dh.f(r), h_len, 0,
                      dy.f(r), static_cast<int64_t>(ylen), static_cast<int>(bc[r]),
                      c->main[r]));
-    VS_TRY(d2h(c->dev[r], y + bb[r] * ylen, dy.f(r), yb[r], c->main[r]));
+    return d2h(c->dev[r], y + bb[r] * ylen, dy.f(r), yb[r], c->main[r]);
+  }));
+  return vs_dist_synchronize(c);
+}
+
+// Data-parallel batches of the wavelet transforms and of independent GEMMs:
+// rows (matrices) sharded over ranks with vs_dist_shard, no communication.
+vs_status vs_dist_swt_batch(vs_dist_t c, int type, int order, int levels, int ext,
+                            const float *x, int len, int batch, float *hi, float *lo) {
+  clear_error();
+  VS_TRY(check_ctx(c));
+  VS_REQUIRE(x && hi && lo, "vs_dist_swt_batch: null pointer");
+  VS_REQUIRE(len > 0 && batch > 0 && levels >= 1, "vs_dist_swt_batch: bad shape");
+  const int R = c->n;
+  std::vector<size_t> bb(R), bc(R), xb(R), hb(R);
+  for (int r = 0; r < R; r++) {
+    vs_dist_shard(batch, R, r, &bb[r], &bc[r]);
+    xb[r] = bc[r] * len * sizeof(float);
+    hb[r] = xb[r] * levels;
   }
+  RankBuffers dx, dhi, dlo;
+  VS_TRY(dx.alloc(c, xb));
+  VS_TRY(dhi.alloc(c, hb));
+  VS_TRY(dlo.alloc(c, xb));
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    if (bc[r] == 0) return VS_OK;
+    VS_TRY(h2d(c->dev[r], dx.f(r), x + bb[r] * len, xb[r], c->main[r]));
+    VS_TRY(vs_swt_multilevel(type, order, levels, ext, dx.f(r), len, dhi.f(r), dlo.f(r),
+                             static_cast<int>(bc[r]), c->main[r]));
+    VS_TRY(d2h(c->dev[r], hi + bb[r] * levels * len, dhi.f(r), hb[r], c->main[r]));
+    return d2h(c->dev[r], lo + bb[r] * len, dlo.f(r), xb[r], c->main[r]);
+  }));
+  return vs_dist_synchronize(c);
+}
+
+vs_status vs_dist_swt_batch_device(vs_dist_t c, int type, int order, int levels, int ext,
+                                   const float *const *x, int len, const int *batch,
+                                   float *const *hi, float *const *lo) {
+  clear_error();
+  VS_TRY(check_ctx(c));
+  VS_REQUIRE(x && hi && lo && batch, "vs_dist_swt_batch_device: null pointer");
+  for (int r = 0; r < c->n; r++) {
+    if (batch[r] == 0) continue;
+    VS_REQUIRE(x[r] && hi[r] && lo[r], "vs_dist_swt_batch_device: rank %d null pointer", r);
+    DevGuard g(c->dev[r]);
+    VS_TRY(vs_swt_multilevel(type, order, levels, ext, x[r], len, hi[r], lo[r], batch[r],
+                             c->main[r]));
+  }
+  return VS_OK;
+}
+
+vs_status vs_dist_dwt_batch(vs_dist_t c, int type, int order, int levels, int ext,
+                            const float *x, int len, int batch, float *out) {
+  clear_error();
+  VS_TRY(check_ctx(c));
+  VS_REQUIRE(x && out, "vs_dist_dwt_batch: null pointer");
+  VS_REQUIRE(len > 0 && batch > 0 && levels >= 1, "vs_dist_dwt_batch: bad shape");
+  const int R = c->n;
+  std::vector<size_t> bb(R), bc(R), xb(R);
+  for (int r = 0; r < R; r++) {
+    vs_dist_shard(batch, R, r, &bb[r], &bc[r]);
+    xb[r] = bc[r] * len * sizeof(float);
+  }
+  RankBuffers dx, dout;
+  VS_TRY(dx.alloc(c, xb));
+  VS_TRY(dout.alloc(c, xb));
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    if (bc[r] == 0) return VS_OK;
+    VS_TRY(h2d(c->dev[r], dx.f(r), x + bb[r] * len, xb[r], c->main[r]));
+    VS_TRY(vs_dwt_multilevel(type, order, levels, ext, dx.f(r), len, dout.f(r),
+                             static_cast<int>(bc[r]), c->main[r]));
+    return d2h(c->dev[r], out + bb[r] * len, dout.f(r), xb[r], c->main[r]);
+  }));
+  return vs_dist_synchronize(c);
+}
+
+vs_status vs_dist_sgemm_batch(vs_dist_t c, int trans_a, int trans_b, int m, int n, int k,
+                              const float *A, const float *B, float *C, int batch) {
+  clear_error();
+  VS_TRY(check_ctx(c));
+  VS_REQUIRE(A && B && C, "vs_dist_sgemm_batch: null pointer");
+  VS_REQUIRE(m > 0 && n > 0 && k > 0 && batch > 0, "vs_dist_sgemm_batch: bad shape");
+  const int R = c->n;
+  const size_t mk = static_cast<size_t>(m) * k, kn = static_cast<size_t>(k) * n,
+               mn = static_cast<size_t>(m) * n;
+  std::vector<size_t> bb(R), bc(R), ab(R), bbytes(R), cb(R);
+  for (int r = 0; r < R; r++) {
+    vs_dist_shard(batch, R, r, &bb[r], &bc[r]);
+    ab[r] = bc[r] * mk * sizeof(float);
+    bbytes[r] = bc[r] * kn * sizeof(float);
+    cb[r] = bc[r] * mn * sizeof(float);
+  }
+  RankBuffers dA, dB, dC;
+  VS_TRY(dA.alloc(c, ab));
+  VS_TRY(dB.alloc(c, bbytes));
+  VS_TRY(dC.alloc(c, cb));
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    if (bc[r] == 0) return VS_OK;
+    VS_TRY(h2d(c->dev[r], dA.f(r), A + bb[r] * mk, ab[r], c->main[r]));
+    VS_TRY(h2d(c->dev[r], dB.f(r), B + bb[r] * kn, bbytes[r], c->main[r]));
+    VS_TRY(vs_sgemm_strided_batched(trans_a, trans_b, m, n, k, 1.f, dA.f(r),
+                                    trans_a ? m : k, static_cast<int64_t>(mk), dB.f(r),
+                                    trans_b ? k : n, static_cast<int64_t>(kn), 0.f, dC.f(r), n,
+                                    static_cast<int64_t>(mn), static_cast<int>(bc[r]),
+                                    c->main[r]));
+    return d2h(c->dev[r], C + bb[r] * mn, dC.f(r), cb[r], c->main[r]);
+  }));
   return vs_dist_synchronize(c);
 }
 
@@ -687,20 +838,21 @@ vs_status vs_dist_conv1d_long(vs_dist_t c, int correlate, const float *x, size_t
   std::vector<const float *> src(R);
   std::vector<float *> halo(R);
   for (int r = 0; r < R; r++) {
-    VS_TRY(h2d(c->dev[r], xb.f(r) + H, x + b[r], cnt[r] * sizeof(float), c->main[r]));
-    VS_TRY(h2d(c->dev[r], dh.f(r), h, h_len * sizeof(float), c->main[r]));
     src[r] = xb.f(r) + H;
     halo[r] = xb.f(r);
   }
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    VS_TRY(h2d(c->dev[r], xb.f(r) + H, x + b[r], cnt[r] * sizeof(float), c->main[r]));
+    return h2d(c->dev[r], dh.f(r), h, h_len * sizeof(float), c->main[r]);
+  }));
   VS_TRY(halo_on(c, c->main, src.data(), cnt.data(), halo.data(), H, +1, 0));
-  for (int r = 0; r < R; r++) {
-    DevGuard g(c->dev[r]);
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
     const int xl = static_cast<int>(H + cnt[r]);
     VS_TRY(vs_conv1d(VS_CONV_AUTO, correlate, xb.f(r), xl, xl, dh.f(r), h_len, 0, yb.f(r),
                      xl + h_len - 1, 1, c->main[r]));
     const size_t keep = cnt[r] + (r == R - 1 ? H : 0);
-    VS_TRY(d2h(c->dev[r], y + b[r], yb.f(r) + H, keep * sizeof(float), c->main[r]));
-  }
+    return d2h(c->dev[r], y + b[r], yb.f(r) + H, keep * sizeof(float), c->main[r]);
+  }));
   return vs_dist_synchronize(c);
 }
 
@@ -724,10 +876,15 @@ vs_status vs_dist_swt_long(vs_dist_t c, int type, int order, int levels, int ext
   std::vector<size_t> sz(R);
   for (int r = 0; r < R; r++) sz[r] = (cnt[r] + Hmax) * sizeof(float);
   VS_TRY(cur.alloc(c, sz));
-  VS_TRY(ohi.alloc(c, sz));
+  {
+    std::vector<size_t> two(R);
+    for (int r = 0; r < R; r++) two[r] = 2 * sz[r];
+    VS_TRY(ohi.alloc(c, two));
+  }
   VS_TRY(olo.alloc(c, sz));
-  for (int r = 0; r < R; r++)
-    VS_TRY(h2d(c->dev[r], cur.f(r), x + b[r], cnt[r] * sizeof(float), c->main[r]));
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    return h2d(c->dev[r], cur.f(r), x + b[r], cnt[r] * sizeof(float), c->main[r]);
+  }));
   for (int l = 1; l <= levels; l++) {
     const size_t H = static_cast<size_t>(order - 1) << (l - 1);
     std::vector<const float *> src(R);
@@ -738,20 +895,31 @@ vs_status vs_dist_swt_long(vs_dist_t c, int type, int order, int levels, int ext
     }
     // the last rank's halo only matters when periodic (else local extension)
     VS_TRY(halo_on(c, c->main, src.data(), cnt.data(), halo.data(), H, -1, periodic ? 1 : 0));
-    for (int r = 0; r < R; r++) {
-      DevGuard g(c->dev[r]);
+    // the level's kernel and the hand-over to the next level go on the main
+    // stream; the band's download follows on the side stream, so it overlaps
+    // the next level's halo exchange and kernel
+    VS_TRY(for_ranks(c, [&](int r) -> vs_status {
       const bool local_ext = r == R - 1 && !periodic;
       const int n = static_cast<int>(local_ext ? cnt[r] : cnt[r] + H);
-      VS_TRY(vs_swt(type, order, l, local_ext ? ext : EXTENSION_TYPE_ZERO, cur.f(r), n, n, ohi.f(r), olo.f(r),
-                    n, 1, c->main[r]));
-      VS_TRY(d2h(c->dev[r], hi + (l - 1) * len + b[r], ohi.f(r), cnt[r] * sizeof(float),
-                 c->main[r]));
+      // ohi alternates between two halves per level: level l's download may
+      // still read its half while level l + 1's kernel writes the other
+      float *oh = ohi.f(r) + (l & 1) * (cnt[r] + Hmax);
+      VS_TRY(vs_swt(type, order, l, local_ext ? ext : EXTENSION_TYPE_ZERO, cur.f(r), n, n, oh,
+                    olo.f(r), n, 1, c->main[r]));
       VS_HIP(hipMemcpyAsync(cur.f(r), olo.f(r), cnt[r] * sizeof(float),
                             hipMemcpyDeviceToDevice, c->main[r]));
-    }
+      EventList done;
+      VS_TRY(done.record(c->main[r]));
+      VS_HIP(hipStreamWaitEvent(c->side[r], done.ev[0], 0));
+      VS_TRY(d2h(c->dev[r], hi + (l - 1) * len + b[r], oh, cnt[r] * sizeof(float),
+                 c->side[r]));
+      VS_HIP(hipStreamSynchronize(c->side[r]));
+      return VS_OK;
+    }));
   }
-  for (int r = 0; r < R; r++)
-    VS_TRY(d2h(c->dev[r], lo + b[r], cur.f(r), cnt[r] * sizeof(float), c->main[r]));
+  VS_TRY(for_ranks(c, [&](int r) -> vs_status {
+    return d2h(c->dev[r], lo + b[r], cur.f(r), cnt[r] * sizeof(float), c->main[r]);
+  }));
   return vs_dist_synchronize(c);
 }
 

@@ -108,6 +108,27 @@ vs_status vs_dist_sgemm_rowsplit_device(vs_dist_t ctx, int m, int n, int k,
 vs_status vs_dist_conv1d_batch(vs_dist_t ctx, int correlate, const float *x,
                                int x_len, const float *h, int h_len, float *y,
                                int batch);
+/// Data-parallel batches, rows (matrices) sharded over ranks with
+/// vs_dist_shard, no communication.  Stationary wavelet transform of
+/// x [batch][len]: hi [batch][levels][len], lo [batch][len] (the layout of
+/// vs_swt_multilevel; reference src/wavelet.c:1907-1940, one signal and one
+/// level per call).
+vs_status vs_dist_swt_batch(vs_dist_t ctx, int type, int order, int levels, int ext,
+                            const float *x, int len, int batch, float *hi, float *lo);
+/// Device-resident form: x[r] / hi[r] / lo[r] are rank r's rows on its
+/// device, batch[r] its row count; enqueued on the ranks' main streams
+/// (vs_dist_synchronize or vs_dist_stream to order after it).
+vs_status vs_dist_swt_batch_device(vs_dist_t ctx, int type, int order, int levels, int ext,
+                                   const float *const *x, int len, const int *batch,
+                                   float *const *hi, float *const *lo);
+/// Decimated pyramid of x [batch][len]: out [batch][len] rows
+/// [hi_1 | hi_2 | ... | hi_L | lo_L] (vs_dwt_multilevel).
+vs_status vs_dist_dwt_batch(vs_dist_t ctx, int type, int order, int levels, int ext,
+                            const float *x, int len, int batch, float *out);
+/// C[b] = op(A[b]) op(B[b]) for b < batch, the matrices sharded over ranks
+/// (A [batch][m][k] or [batch][k][m] when trans_a, B likewise, C [batch][m][n]).
+vs_status vs_dist_sgemm_batch(vs_dist_t ctx, int trans_a, int trans_b, int m, int n, int k,
+                              const float *A, const float *B, float *C, int batch);
 /// Context-parallel convolution / correlation of one long signal: x split
 /// into contiguous chunks (each >= h_len - 1), rank r receives the last
 /// h_len - 1 samples of rank r-1 as history and writes its disjoint slice of

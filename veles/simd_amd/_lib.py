@@ -117,6 +117,10 @@ _SIGNATURES = {
     "vs_dist_sgemm_rowsplit_device": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i]),
     "vs_dist_conv1d_batch": (_i, [_vp, _i, _vp, _i, _vp, _i, _vp, _i]),
     "vs_dist_conv1d_long": (_i, [_vp, _i, _vp, _sz, _vp, _i, _vp]),
+    "vs_dist_swt_batch": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
+    "vs_dist_swt_batch_device": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
+    "vs_dist_dwt_batch": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "vs_dist_sgemm_batch": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i]),
     "vs_dist_swt_long": (_i, [_vp, _i, _i, _i, _i, _vp, _sz, _vp, _vp]),
 }
 

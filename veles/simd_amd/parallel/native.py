@@ -173,6 +173,59 @@ class DeviceGroup:
                    "vs_dist_conv1d_batch")
         return y
 
+    def swt_batch(self, x, wavelet: str = "daubechies", order: int = 8, levels: int = 1,
+                  ext: str = "periodic") -> tuple[np.ndarray, np.ndarray]:
+        """Data-parallel stationary wavelet transform of the rows of x
+        [batch, len]: (hi [batch, levels, len], lo [batch, len])."""
+        x = _f32(x)
+        batch, n = x.shape
+        hi = np.empty((batch, levels, n), np.float32)
+        lo = np.empty((batch, n), np.float32)
+        _lib.check(_lib.lib().vs_dist_swt_batch(self._h, WAVELETS[wavelet], order, levels,
+                                                EXTENSIONS[ext], _ptr(x), n, batch, _ptr(hi),
+                                                _ptr(lo)), "vs_dist_swt_batch")
+        return hi, lo
+
+    def swt_batch_device(self, x, hi, lo, wavelet: str = "daubechies", order: int = 8,
+                         levels: int = 1, ext: str = "periodic") -> None:
+        """Device-resident data-parallel SWT: x[r] [rows_r, len], hi[r]
+        [rows_r, levels, len], lo[r] [rows_r, len] are rank r's tensors on its
+        device; enqueued on the ranks' streams and synchronised."""
+        n = x[0].shape[-1]
+        counts = (ctypes.c_int * len(x))(*[t.shape[0] for t in x])
+        self._sync_inputs(list(x))
+        _lib.check(_lib.lib().vs_dist_swt_batch_device(
+            self._h, WAVELETS[wavelet], order, levels, EXTENSIONS[ext],
+            _ptr_array([t.data_ptr() for t in x]), n, counts,
+            _ptr_array([t.data_ptr() for t in hi]), _ptr_array([t.data_ptr() for t in lo])),
+            "vs_dist_swt_batch_device")
+        self.synchronize()
+
+    def dwt_batch(self, x, wavelet: str = "daubechies", order: int = 8, levels: int = 1,
+                  ext: str = "periodic") -> np.ndarray:
+        """Data-parallel decimated pyramid of the rows of x [batch, len]:
+        rows [hi_1 | hi_2 | ... | hi_L | lo_L]."""
+        x = _f32(x)
+        batch, n = x.shape
+        out = np.empty((batch, n), np.float32)
+        _lib.check(_lib.lib().vs_dist_dwt_batch(self._h, WAVELETS[wavelet], order, levels,
+                                                EXTENSIONS[ext], _ptr(x), n, batch, _ptr(out)),
+                   "vs_dist_dwt_batch")
+        return out
+
+    def sgemm_batch(self, a, b, trans_a: bool = False, trans_b: bool = False) -> np.ndarray:
+        """Data-parallel batched C[i] = op(A[i]) op(B[i]), matrices sharded
+        over ranks."""
+        a, b = _f32(a), _f32(b)
+        batch = a.shape[0]
+        m, k = (a.shape[2], a.shape[1]) if trans_a else (a.shape[1], a.shape[2])
+        n = b.shape[1] if trans_b else b.shape[2]
+        c = np.empty((batch, m, n), np.float32)
+        _lib.check(_lib.lib().vs_dist_sgemm_batch(self._h, int(trans_a), int(trans_b), m, n, k,
+                                                  _ptr(a), _ptr(b), _ptr(c), batch),
+                   "vs_dist_sgemm_batch")
+        return c
+
     def conv1d_long(self, x, h, correlate: bool = False) -> np.ndarray:
         x, h = _f32(x), _f32(h)
         y = np.empty(x.size + h.size - 1, np.float32)
