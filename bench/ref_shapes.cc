@@ -14,6 +14,7 @@
 // (vs_* API), i.e. the throughput a GPU caller sees.
 // Output: one JSON object, microseconds per call.
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -111,6 +112,26 @@ void matrix_rows(int scale) {
        }));
   emit("matrix_multiply_scalar_300x256x1000",
        time_us(2, [&] { matrix_multiply(0, a.data(), b.data(), w1, h1, w2, w1, c.data()); }));
+#ifdef VELES_DEVICE
+  // the same calls on page-locked operands from vs_host_alloc
+  float *pa = static_cast<float *>(vs_host_alloc(a.size() * sizeof(float)));
+  float *pb = static_cast<float *>(vs_host_alloc(b.size() * sizeof(float)));
+  float *pbt = static_cast<float *>(vs_host_alloc(bt.size() * sizeof(float)));
+  float *pc = static_cast<float *>(vs_host_alloc(c.size() * sizeof(float)));
+  if (!pa || !pb || !pbt || !pc) return;
+  std::copy(a.begin(), a.end(), pa);
+  std::copy(b.begin(), b.end(), pb);
+  std::copy(bt.begin(), bt.end(), pbt);
+  emit("matrix_multiply_pinned_300x256x1000",
+       time_us(it * 5, [&] { matrix_multiply(1, pa, pb, w1, h1, w2, w1, pc); }));
+  emit("matrix_multiply_transposed_pinned_300x256x1000", time_us(it * 5, [&] {
+         matrix_multiply_transposed(1, pa, pbt, w1, h1, w1, w2, pc);
+       }));
+  vs_host_free(pc);
+  vs_host_free(pa);
+  vs_host_free(pb);
+  vs_host_free(pbt);
+#endif
 }
 
 void wavelet_rows(int scale) {
@@ -158,6 +179,22 @@ void floor_rows() {
   std::vector<float> a(4, 1.f), b(4, 2.f), c(4);
   emit("floor_host_api_matrix_add_2x2",
        time_us(20000, [&] { matrix_add(1, a.data(), b.data(), 2, 2, c.data()); }));
+  {  // the PCIe share of the 300x256 . 256x1000 host call: A and B in, C out
+    const size_t in_b = (300 * 256 + 256 * 1000) * sizeof(float), out_b = 300 * 1000 * sizeof(float);
+    void *hin = vs_host_alloc(in_b), *hout = vs_host_alloc(out_b), *din = nullptr, *dout = nullptr;
+    hipMalloc(&din, in_b);
+    hipMalloc(&dout, out_b);
+    if (hin && hout && din && dout)
+      emit("floor_pcie_pinned_1.33MB_in_1.2MB_out", time_us(500, [&] {
+             hipMemcpyAsync(din, hin, in_b, hipMemcpyHostToDevice, s);
+             hipMemcpyAsync(hout, dout, out_b, hipMemcpyDeviceToHost, s);
+             wait();
+           }));
+    hipFree(din);
+    hipFree(dout);
+    vs_host_free(hin);
+    vs_host_free(hout);
+  }
   for (int algo : {VS_CONV_DIRECT, VS_CONV_FFT}) {
     float *x, *h, *y;
     hipMalloc(&x, 4 * 512);

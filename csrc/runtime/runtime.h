@@ -197,6 +197,7 @@ class Staged {
   DeviceBuffer buf_;
   vs_status status_ = VS_OK;
   bool packed_ = false;  // lives in the call's CallStaging arena
+  bool pinned_ = false;  // pinned host operand on the DMA / in-place path
 };
 
 // Waits for everything queued on `s` so far by polling an event (lower

@@ -204,3 +204,47 @@ def test_sgemm_default_large_paths(m, n, k):
     c = ops.sgemm(a, b)
     ref = a.double() @ b.double()
     assert (c.double() - ref).abs().max().item() < 2e-6 * k
+
+
+@pytest.mark.gpu
+def test_host_api_pinned_operands_match_pageable():
+    """Page-locked operands (vs_host_alloc) take the DMA / in-place staging
+    path: same result as the pageable call, bit for bit (same kernel, same
+    data)."""
+    h1, w1, w2 = 300, 256, 1000
+    rng = np.random.default_rng(11)
+    a = rng.standard_normal(h1 * w1).astype(np.float32)
+    b = rng.standard_normal(w1 * w2).astype(np.float32)
+    bt = np.ascontiguousarray(b.reshape(w1, w2).T).ravel()
+    want = capi.matrix_multiply(1, a, b, w1, h1, w2, w1)
+    pins = [capi.PinnedArray(n) for n in (a.size, b.size, bt.size, h1 * w2)]
+    try:
+        pa, pb, pbt, got = (q.array for q in pins)
+        pa[:], pb[:], pbt[:] = a, b, bt
+        for _ in range(3):  # repeated calls reuse the mapping
+            got[:] = np.nan
+            capi.fn("matrix_multiply")(1, capi.p(pa), capi.p(pb), w1, h1, w2, w1, capi.p(got))
+            np.testing.assert_array_equal(got, want)
+        got[:] = np.nan
+        capi.fn("matrix_multiply_transposed")(1, capi.p(pa), capi.p(pbt), w1, h1, w1, w2,
+                                              capi.p(got))
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-4)
+        # mixed: pinned inputs, pageable output
+        np.testing.assert_array_equal(capi.matrix_multiply(1, pa, pb, w1, h1, w2, w1), want)
+    finally:
+        for q in pins:
+            q.close()
+
+
+@pytest.mark.gpu
+def test_host_api_pinned_convolve():
+    """A long pinned signal through the host convolution API."""
+    n, m = 1 << 18, 257
+    rng = np.random.default_rng(12)
+    x = rng.standard_normal(n).astype(np.float32)
+    h = rng.standard_normal(m).astype(np.float32)
+    want = capi.convolve_simd(1, x, h)
+    with capi.PinnedArray(n) as px:
+        px[:] = x
+        got = capi.convolve_simd(1, px, h)
+    np.testing.assert_array_equal(got, want)

@@ -42,6 +42,8 @@ _SIGNATURES = {
     "vs_is_device_pointer": (_i, [_vp]),
     "vs_stream_synchronize": (_i, [_vp]),
     "vs_compiled_arch": (_i, []),
+    "vs_host_alloc": (_vp, [_sz]),
+    "vs_host_free": (None, [_vp]),
     "vs_convert": (_i, [_vp, _i, _vp, _i, _sz, _vp]),
     "vs_binary": (_i, [_i, _vp, _vp, _vp, _sz, _vp]),
     "vs_complex_multiply": (_i, [_vp, _vp, _vp, _sz, _i, _vp]),

@@ -143,6 +143,32 @@ def f32(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
+class PinnedArray:
+    """A float32 numpy array in page-locked memory from vs_host_alloc: the
+    host API reads and writes such operands by DMA (or in place) instead of
+    through the pageable staging copies.  Keep the object alive while the
+    array is in use; close() (or the context manager) frees the memory."""
+
+    def __init__(self, n: int):
+        self._ptr = _lib.lib().vs_host_alloc(n * 4)
+        if not self._ptr:
+            raise MemoryError(f"vs_host_alloc({n * 4}) failed")
+        buf = (ctypes.c_float * n).from_address(self._ptr)
+        self.array = np.frombuffer(buf, dtype=np.float32, count=n)
+
+    def close(self):
+        if self._ptr:
+            self.array = None
+            _lib.lib().vs_host_free(self._ptr)
+            self._ptr = None
+
+    def __enter__(self):
+        return self.array
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 # ------------------------------------------------------------------ helpers
 def matrix_multiply(simd, m1, m2, w1, h1, w2, h2):
     m1, m2 = f32(m1), f32(m2)
