@@ -9,6 +9,8 @@
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include "simd/convolve.h"
 
+#include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 
@@ -27,9 +29,9 @@ struct ConvPlan {
   int block;      // transform length (informational)
 };
 
-int next_pow2_ge(size_t n) {
+int next_pow2_ge(size_t n) {  // saturates at 2^30 (the handles' int field)
   int p = 1;
-  while (static_cast<size_t>(p) < n) p <<= 1;
+  while (static_cast<size_t>(p) < n && p < (1 << 30)) p <<= 1;
   return p;
 }
 
@@ -38,7 +40,6 @@ using vs::api::checked_int;
 void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl,
               const float *h, size_t hl, float *result) {
   const size_t yl = xl + hl - 1;
-  (void)checked_int(what, yl);
   // Small direct convolutions run the tap-split kernel (conv.hip), whose
   // workgroups load their input window once with every load in flight:
   // their inputs are read zero-copy from the pinned staging arena (no
@@ -52,7 +53,9 @@ void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl
     VS_TRY(y.status());
     VS_TRY(xx.status());
     VS_TRY(hh.status());
-    VS_TRY(vs_conv1d(algo, reverse, xx.dev<float>(), checked_int(what, xl),
+    // signals of any length (vs_conv1d cuts rows of 2^29 outputs or more into
+    // pieces); only the filter length is bounded
+    VS_TRY(vs_conv1d(algo, reverse, xx.dev<float>(), static_cast<int64_t>(xl),
                      static_cast<int64_t>(xl), hh.dev<float>(), checked_int(what, hl),
                      0, y.dev<float>(), static_cast<int64_t>(yl), 1, s));
     return y.finish();
@@ -90,7 +93,8 @@ ConvolutionFFTHandle fft_init(size_t xl, size_t hl, int reverse) {
   h.fft_inverse_plan = p;
   h.M = static_cast<int *>(std::malloc(sizeof(int)));
   *h.M = p->block;
-  h.x_length = checked_int("convolve_fft_initialize", xl);
+  // the reference's int fields saturate; the plan keeps the exact lengths
+  h.x_length = static_cast<int>(std::min<size_t>(xl, INT_MAX));
   h.h_length = checked_int("convolve_fft_initialize", hl);
   h.inputs = nullptr;
   h.reverse = reverse;
@@ -127,12 +131,15 @@ void os_fini(ConvolutionOverlapSaveHandle h) {
 ConvolutionHandle auto_init(size_t xl, size_t hl, int reverse) {
   ConvolutionHandle h;
   std::memset(&h, 0, sizeof(h));
-  h.x_length = checked_int("convolve_initialize", xl);
+  h.x_length = static_cast<int>(std::min<size_t>(xl, INT_MAX));
   h.h_length = checked_int("convolve_initialize", hl);
   int algo;
   if (vs::gpu_available()) {
-    algo = vs_conv1d_select(h.x_length, h.h_length, 1);
+    algo = vs_conv1d_select(static_cast<int64_t>(xl), h.h_length, 1);
     if (algo == VS_CONV_OVERLAP_SAVE && !(hl < xl / 2)) algo = VS_CONV_FFT;
+    // the brute-force handle has only the int length fields: longer signals
+    // take a handle with a plan
+    if (algo == VS_CONV_DIRECT && xl > static_cast<size_t>(INT_MAX)) algo = VS_CONV_OVERLAP_SAVE;
   } else {
     // reference heuristic (src/convolve.c:349-363)
     if (xl > hl * 2)

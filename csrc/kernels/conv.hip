@@ -35,7 +35,7 @@
 
 namespace vs {
 namespace conv {
-extern int g_conv_buf, g_conv_real, g_conv_real_all, g_conv_fused4;  // tuning knobs, defined below
+extern thread_local int g_conv_buf, g_conv_real, g_conv_real_all, g_conv_fused4;  // tuning knobs, defined below
 namespace {
 
 using fft::cmul;
@@ -44,8 +44,6 @@ using fft::reg_index;
 
 // smallest real-block transform (L = 2^kRealMinLog real samples, M = L / 2)
 constexpr int kRealMinLog = 7;
-// taps per partition of a filter too long for one overlap-save block
-constexpr int kPartTaps = 4096;
 
 // ------------------------------------------------------------- direct
 constexpr int kDirThreads = 256;
@@ -753,22 +751,27 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())
 // before the first butterfly).
 template <int LOGM>
 __global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
-    const float *__restrict__ h, int hlen, int64_t hs, int reverse,
+    const float *__restrict__ h, int hlen, int64_t hs, int reverse, int part_taps,
     const float2 *__restrict__ tw, const float2 *__restrict__ twl, float4 *__restrict__ PQ) {
   using PL = Plan<LOGM>;
   constexpr int E = PL::E;
   __shared__ float2 lds[PL::kLds];
   const int t = threadIdx.x;
-  const float *hr = h + static_cast<long long>(blockIdx.x) * hs;
+  // grid = (partitions of part_taps taps, filters): partition p holds taps
+  // [p part_taps, (p + 1) part_taps) of the (reversed) filter
+  const float *hr = h + static_cast<long long>(blockIdx.y) * hs;
+  const int p0 = static_cast<int>(blockIdx.x) * part_taps;
+  const int taps = min(part_taps, hlen - p0);
   constexpr int R0 = PL::first_radix(false);
   constexpr int RL = PL::last_radix(false);
   float2 v[E], wk[E];
 #pragma unroll
   for (int e = 0; e < E; e++) {
     const int n = 2 * reg_index<PL, R0>(t, e / R0, e % R0);
-    const int i0 = reverse ? hlen - 1 - n : n, i1 = reverse ? hlen - 2 - n : n + 1;
-    const float u0 = hr[n < hlen ? i0 : 0], u1 = hr[n + 1 < hlen ? i1 : 0];
-    v[e] = make_float2(n < hlen ? u0 : 0.f, n + 1 < hlen ? u1 : 0.f);
+    const int g = p0 + n;  // tap index in the (reversed) filter
+    const int i0 = reverse ? hlen - 1 - g : g, i1 = reverse ? hlen - 2 - g : g + 1;
+    const float u0 = hr[n < taps ? i0 : 0], u1 = hr[n + 1 < taps ? i1 : 0];
+    v[e] = make_float2(n < taps ? u0 : 0.f, n + 1 < taps ? u1 : 0.f);
   }
 #pragma unroll
   for (int e = 0; e < E; e++) wk[e] = twl[reg_index<PL, RL>(t, e / RL, e % RL)];
@@ -779,7 +782,7 @@ __global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
 #pragma unroll
   for (int e = 0; e < E; e++) lds[fft::slot<PL>(reg_index<PL, RL>(t, e / RL, e % RL))] = v[e];
   fft::lds_barrier();
-  float4 *out = PQ + static_cast<long long>(blockIdx.x) * PL::N;
+  float4 *out = PQ + (static_cast<long long>(blockIdx.y) * gridDim.x + blockIdx.x) * PL::N;
   const float sc = 1.0f / static_cast<float>(PL::N);
 #pragma unroll
   for (int e = 0; e < E; e++) {
@@ -803,17 +806,20 @@ __global__ __launch_bounds__((Plan<LOGM>::TPS)) void real_filter_kernel(
 }
 
 // P / Q of nfilt filters (stride hs) for the L = 2^(LOGM+1) real block into
-// `pq` (PL::N float4 per filter).
+// `pq`: per filter, one table of PL::N float4 for each partition of
+// part_taps taps (a filter that fits one block: part_taps = hlen).
 template <int LOGM>
 vs_status launch_real_filter(int correlate, const float *h, int hlen, int64_t hs, int nfilt,
-                             float4 *pq, hipStream_t s) {
+                             float4 *pq, hipStream_t s, int part_taps = 0) {
   vs_status st;
   const float2 *tw = fft::twiddles(LOGM, &st);
   if (!tw) return st;
   const float2 *twl = fft::twiddles(LOGM + 1, &st);
   if (!twl) return st;
-  hipLaunchKernelGGL((real_filter_kernel<LOGM>), dim3(static_cast<unsigned>(nfilt)),
-                     dim3(Plan<LOGM>::TPS), 0, s, h, hlen, hs, correlate, tw, twl, pq);
+  if (part_taps <= 0) part_taps = hlen;
+  const unsigned parts = static_cast<unsigned>((hlen + part_taps - 1) / part_taps);
+  hipLaunchKernelGGL((real_filter_kernel<LOGM>), dim3(parts, static_cast<unsigned>(nfilt)),
+                     dim3(Plan<LOGM>::TPS), 0, s, h, hlen, hs, correlate, part_taps, tw, twl, pq);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
@@ -842,6 +848,135 @@ vs_status run_real_t(int correlate, const float *h, int hlen, int64_t hs, int nf
     hipLaunchKernelGGL((real_conv_kernel<LOGM, EP, false>), grid, dim3(PL::TPS), 0, s, a, tw);
   VS_HIP(hipGetLastError());
   return VS_OK;
+}
+
+// ------------------------- uniformly partitioned overlap-save (long filters)
+// Filters longer than one overlap-save block (reference src/convolve.c:116-121
+// sizes one block from the filter; :181-228 is its block loop): the filter is
+// cut into partitions of B = L / 2 taps and the signal into blocks of L
+// samples every B (frequency-domain delay line).  Each signal block is
+// transformed once (fdl_forward_kernel: its packed M = B point spectrum Z_s
+// goes to memory), the products are accumulated in the spectral domain,
+//   Y_b[k] = sum_p P_p[k] Z_{b-p}[k] + Q_p[k] conj(Z_{b-p}[M - k]),
+// with the partitions' P / Q tables of the real-block kernel
+// (fdl_mac_kernel), and each output block takes one inverse transform
+// (fdl_inverse_kernel) -- against one forward and one inverse transform per
+// block and partition when every partition runs its own overlap-save pass.
+template <int LOGM, int EP, bool BUF>
+__global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())) void fdl_forward_kernel(
+    RealArgs a, float2 *__restrict__ Z, const float2 *__restrict__ tw) {
+  using PL = Plan<LOGM, EP>;
+  constexpr int E = PL::E;
+  __shared__ float2 lds[PL::kLds];
+  const int t = threadIdx.x;
+  const int sig = blockIdx.y;
+  const int blk = blockIdx.x;
+  const float *xr = a.x + static_cast<long long>(sig) * a.xs;
+  const int st = blk * a.step - a.pre;
+  float2 v[E];
+  load_real<PL, BUF>(a, xr, st, t, v);
+  fft::RegTw<PL, false> twf;
+  twf.load(t, tw);
+  __builtin_amdgcn_sched_barrier(0);
+  fft::transform<PL, false, false>(v, lds, t, twf);
+  constexpr int RL = PL::last_radix(false);
+  float2 *z = Z + (static_cast<long long>(sig) * gridDim.x + blk) * PL::N;
+#pragma unroll
+  for (int b = 0; b < E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++) z[reg_index<PL, RL>(t, b, j)] = v[b * RL + j];
+}
+
+template <int LOGM, int EP, bool BUF>
+__global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())) void fdl_inverse_kernel(
+    RealArgs a, const float2 *__restrict__ Y, const float2 *__restrict__ tw) {
+  using PL = Plan<LOGM, EP>;
+  constexpr int E = PL::E;
+  __shared__ float2 lds[PL::kLds];
+  const int t = threadIdx.x;
+  const int sig = blockIdx.y;
+  const int blk = blockIdx.x;
+  float *yr = a.y + static_cast<long long>(sig) * a.ys;
+  const int st = blk * a.step - a.pre;
+  constexpr int RL = PL::last_radix(false);
+  const float2 *ys = Y + (static_cast<long long>(sig) * gridDim.x + blk) * PL::N;
+  float2 v[E];
+#pragma unroll
+  for (int b = 0; b < E / RL; b++)
+#pragma unroll
+    for (int j = 0; j < RL; j++) v[b * RL + j] = ys[reg_index<PL, RL>(t, b, j)];
+  fft::RegTw<PL, true> twi;
+  twi.load(t, tw);
+  __builtin_amdgcn_sched_barrier(0);
+  fft::transform<PL, true, true>(v, lds, t, twi);
+  store_real<PL, BUF>(a, yr, st, t, v);
+}
+
+// Spectral accumulation.  One lane owns the bin pair (k, M - k) of kFdlTile
+// consecutive output blocks of one signal: 2 kFdlTile accumulators.  The
+// partitions go by in groups of kFdlGroup whose P / Q (2 float4 each) stay in
+// registers while the lane walks the source blocks the group needs, so
+// every Z load (16 bytes) feeds up to 4 kFdlGroup complex multiply-adds.
+// Groups of 4 at 64 VGPRs: 0.38 / 0.94 ms for 8 / 25 partitions at 2^20 x 64
+// (about 5 TB/s of Z reads and Y writes); groups of 8 read less but run at
+// two waves per SIMD and lose 7-14 % (profiles/r3/conv/fdl.md).
+constexpr int kFdlTile = 16;
+constexpr int kFdlGroup = 4;
+
+struct FdlMac {
+  const float2 *Z;   // [batch][nsrc][M]
+  const float4 *PQ;  // [filters][parts][M]
+  float2 *Y;         // [batch][nblk][M]
+  int nsrc, nblk, parts, m, pq_per_signal;
+};
+
+__global__ __launch_bounds__(256) void fdl_mac_kernel(FdlMac a) {
+  constexpr int G = kFdlGroup;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j > a.m / 2) return;
+  const int k = j, km = (a.m - j) & (a.m - 1);
+  const long long sig = blockIdx.z;
+  const int b0 = blockIdx.y * kFdlTile;
+  const float2 *Z = a.Z + sig * a.nsrc * a.m;
+  const float4 *PQ = a.PQ + (a.pq_per_signal ? sig * a.parts * a.m : 0);
+  float2 acck[kFdlTile], accm[kFdlTile];
+#pragma unroll
+  for (int i = 0; i < kFdlTile; i++) acck[i] = accm[i] = make_float2(0.f, 0.f);
+  for (int pc = 0; pc < a.parts; pc += G) {
+    float4 pk[G], pm[G];
+#pragma unroll
+    for (int pp = 0; pp < G; pp++) {
+      pk[pp] = pm[pp] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (pc + pp < a.parts) {
+        pk[pp] = PQ[static_cast<long long>(pc + pp) * a.m + k];
+        pm[pp] = PQ[static_cast<long long>(pc + pp) * a.m + km];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kFdlTile + G - 1; i++) {
+      // source block s feeds output b0 + i - (G - 1) + pp through partition pc + pp
+      const int s = b0 - pc - (G - 1) + i;
+      if (s < 0 || s >= a.nsrc) continue;
+      const float2 zk = Z[static_cast<long long>(s) * a.m + k];
+      const float2 zm = Z[static_cast<long long>(s) * a.m + km];
+#pragma unroll
+      for (int pp = 0; pp < G; pp++) {
+        const int o = i - (G - 1) + pp;
+        if (o < 0 || o >= kFdlTile) continue;
+        acck[o] = fft::cadd(acck[o], fft::cadd(cmul(make_float2(pk[pp].x, pk[pp].y), zk),
+                                               fft::cmulc(make_float2(pk[pp].z, pk[pp].w), zm)));
+        accm[o] = fft::cadd(accm[o], fft::cadd(cmul(make_float2(pm[pp].x, pm[pp].y), zm),
+                                               fft::cmulc(make_float2(pm[pp].z, pm[pp].w), zk)));
+      }
+    }
+  }
+  float2 *Y = a.Y + sig * a.nblk * a.m;
+#pragma unroll
+  for (int o = 0; o < kFdlTile; o++) {
+    if (b0 + o >= a.nblk) break;
+    Y[static_cast<long long>(b0 + o) * a.m + k] = acck[o];
+    Y[static_cast<long long>(b0 + o) * a.m + km] = accm[o];
+  }
 }
 
 // ------------------------------------------ large FFT path (four-step)
@@ -892,10 +1027,13 @@ __global__ __launch_bounds__(256) void spectrum_mul_kernel(
 
 }  // namespace
 
+// The tuning knobs are per thread (vs_tune_set changes the calling thread's
+// values only; vs_tune_reset restores the defaults): concurrent callers never
+// see each other's settings, and a plan records what it was built with.
 // Tuning knob (vs_tune_set("os_block_log_max", n)): cap of the overlap-save
 // block size, for A/B measurements.  The real-block kernel reaches one more
 // power of two than the complex transforms (L = 2M real samples).
-int g_os_log_max = fft::kMaxLdsLog + 1;
+thread_local int g_os_log_max = fft::kMaxLdsLog + 1;
 // Tuning knob (vs_tune_set("os_block_extra", 0/2/3/4)): overlap-save block
 // L = 2^(floor(log2 h) + extra); the reference uses 2 (src/convolve.c:116-121).
 // 0 (default): 3 while that keeps L <= 8192, else 2 -- the M <= 4096 real
@@ -903,22 +1041,33 @@ int g_os_log_max = fft::kMaxLdsLog + 1;
 // (x = 2^20 x 64, Msamples/s, profiles/r2/conv_block_rule.md):
 //   h = 700: 344 -> 388 K, 1000: 260 -> 336 K, 2000: 270 -> 330 K;
 //   h = 3000 / 4096 keep L = 8192 / 16384 (L = 16384 / 32768: -7 % / -14 %).
-int g_os_extra = 0;
+thread_local int g_os_extra = 0;
 // Tuning knob (vs_tune_set("conv_fused4", 0/1)): fused three-pass four-step
 // FFT convolution (fft::conv_four_step) vs the seven-pass sequence.
-int g_conv_fused4 = 1;
+thread_local int g_conv_fused4 = 1;
 // Tuning knob (vs_tune_set("conv_buffer", 0/1)): buffer-descriptor loads and
 // stores in the fused block kernels.
-int g_conv_buf = 1;
-// Tuning knob (vs_tune_set("conv_real", 0/1/2)): real-block kernel for the
-// overlap-save / single-block paths (0: pair kernel; 2: 16 points per thread
-// at M = 8192 instead of 32).
-int g_conv_real = 1;
+thread_local int g_conv_buf = 1;
+// Tuning knob (vs_tune_set("conv_real", 0/1)): real-block kernel for the
+// overlap-save / single-block paths (0: pair kernel).
+thread_local int g_conv_real = 1;
 // Tuning knob (vs_tune_set("conv_real_all", 0/1)): real-block kernel for
 // every block size (default: L >= 8192 only, see use_real).
-int g_conv_real_all = 0;
+thread_local int g_conv_real_all = 0;
 
 bool use_real(int logl);
+int fdl_part_taps();
+constexpr int kFdlMaxParts = 12;
+
+// Longest row one kernel launch sequence handles: the buffer-descriptor
+// loads and stores of the block kernels need every byte offset of a row in
+// 31 bits (rows below 2^29 samples).  vs_conv1d cuts longer rows into pieces
+// of 2^28 outputs.
+// vs_tune_set("conv_piece_log", n) lowers the piece size (tests of the piece
+// logic on short rows).
+thread_local int g_piece_log = 28;
+inline long long piece_out() { return 1LL << g_piece_log; }
+inline long long max_call_out() { return 2 * piece_out() - 1; }
 
 // Largest single-workgroup block: the real-block kernel transforms L = 2M
 // real samples as an M-point complex FFT, so it reaches 2^(kMaxLdsLog + 1).
@@ -939,9 +1088,23 @@ int os_block_log(int hlen) {
   return lg;
 }
 
-int select(int xlen, int hlen, int batch) {
+// Overlap-save with one block per filter while >= 28 % of each block is
+// useful output: the block rule keeps >= 75 % up to h = 8192; past that
+// L = 32768 real blocks run ~370 M block points/s at 2^20 x 64 (h = 20000,
+// 39 % useful: 144 Gsamples/s; ~104 at 28 %) against ~104 for three or four filter
+// partitions of the uniformly partitioned path and 70 for the whole-signal
+// four-step FFT (profiles/r2/conv/conv_long.log, profiles/r3/conv/fdl.md).
+bool os_single_block(int hlen) {
+  const int los = os_block_log(hlen);
+  return (1 << los) > hlen - 1 + 16 &&
+         static_cast<long long>((1 << los) - (hlen - 1)) * 100 >= 28LL * (1 << los);
+}
+
+int select(int64_t xlen, int hlen, int batch) {
   const long long ylen = static_cast<long long>(xlen) + hlen - 1;
   (void)batch;
+  // rows cut into pieces (vs_conv1d): no single transform covers them
+  if (ylen > max_call_out()) return hlen <= 8 ? VS_CONV_DIRECT : VS_CONV_OVERLAP_SAVE;
   // Direct only for very short filters or signals: at x = 2^20 x 64 the
   // float4 direct kernel runs h <= 8 at ~650 Gsamples/s against ~490 for
   // overlap-save; at h = 16 they are level (505 vs 500 with 16-byte aligned
@@ -949,27 +1112,27 @@ int select(int xlen, int hlen, int batch) {
   // (profiles/r2/session6/conv_small.md).
   if (ylen <= 64 || hlen <= 8 || (hlen <= 32 && xlen < 4096)) return VS_CONV_DIRECT;
   const int los = os_block_log(hlen);
-  // Overlap-save while >= 20 % of each block is useful output: the block rule
-  // keeps >= 75 % up to h = 8192; past that L = 32768 real blocks (~370 M block
-  // points/s at 2^20 x 64) still beat the whole-signal four-step FFT (fused,
-  // ~73 Gsamples/s) down to ~20 % useful -- h = 20000 (39 %): 144 vs 73
-  // (profiles/r2/conv/conv_long.log, f4_ab.log).
-  const bool os_ok = static_cast<long long>((1 << los) - (hlen - 1)) * 100 >=
-                     20LL * (1 << los);
+  const bool os_ok = os_single_block(hlen);
   int lm = 1;
   while ((1LL << lm) < ylen) lm++;
   if (lm <= max_block_log() && (!os_ok || ylen <= (1LL << los)))
     return VS_CONV_FFT;  // one block covers the whole output
   if (os_ok) return VS_CONV_OVERLAP_SAVE;
-  // Long filter: one padded transform while it exists, else partitioned
-  // overlap-save (vs_conv1d never fails for a valid shape).
-  return lm <= fft::kMaxLog ? VS_CONV_FFT : VS_CONV_OVERLAP_SAVE;
+  // Long filter: uniformly partitioned overlap-save up to kFdlMaxParts
+  // partitions (its spectral accumulation grows with the partition count:
+  // at 2^20 x 64, 8 partitions run 80 Gsamples/s, 25 run 50, the fused
+  // four-step transform 70 whatever the filter), else one padded transform
+  // while it exists (vs_conv1d never fails for a valid shape).
+  const int parts = (hlen + fdl_part_taps() - 1) / fdl_part_taps();
+  return parts <= kFdlMaxParts || lm > fft::kMaxLog ? VS_CONV_OVERLAP_SAVE : VS_CONV_FFT;
 }
 
+// Every run_* entry writes the first `ylen` outputs (<= xlen + hlen - 1) of
+// each row: callers that cut a long signal into pieces drop the tail that
+// the next piece owns.
 vs_status run_direct(int correlate, const float *x, int xlen, int64_t xs,
-                     const float *h, int hlen, int64_t hs, float *y, int64_t ys,
+                     const float *h, int hlen, int64_t hs, float *y, int64_t ys, int ylen,
                      int batch, hipStream_t s) {
-  const int ylen = xlen + hlen - 1;
   const dim3 grid(static_cast<unsigned>((ylen + kDirOut - 1) / kDirOut),
                   static_cast<unsigned>(batch));
   // VEC: x rows 16-byte aligned (float4 window loads); y rows may start
@@ -1014,14 +1177,13 @@ vs_status filter_spectra(int correlate, const float *h, int hlen, int64_t hs,
 
 vs_status run_block(int correlate, bool overlap_save, const float *x, int xlen,
                     int64_t xs, const float *h, int hlen, int64_t hs, float *y,
-                    int64_t ys, int batch, hipStream_t s) {
-  const int ylen = xlen + hlen - 1;
+                    int64_t ys, int ylen, int batch, hipStream_t s) {
   int logl;
   if (overlap_save) {
     logl = os_block_log(hlen);
   } else {
     logl = 4;  // smallest instantiated transform
-    while ((1 << logl) < ylen) logl++;
+    while ((1 << logl) < xlen + hlen - 1) logl++;
   }
   VS_REQUIRE(logl <= fft::kMaxLdsLog, "block convolution: block 2^%d too large", logl);
   const int L = 1 << logl;
@@ -1069,7 +1231,7 @@ vs_status run_block(int correlate, bool overlap_save, const float *x, int xlen,
 // pair kernel skips the spectrum exchange.
 bool use_real(int logl) {
   if (g_conv_real == 0 || logl < kRealMinLog) return false;
-  return g_conv_real == 2 || logl >= 12 || g_conv_real_all;
+  return logl >= 12 || g_conv_real_all;
 }
 
 // Real-block path (real_conv_kernel): blocks of L = 2^logl real samples.
@@ -1078,9 +1240,10 @@ bool use_real(int logl) {
 vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, int64_t xs,
                    const float *h, int hlen, int64_t hs, float *y, int64_t ys, int ylen,
                    int yroom, int accumulate, int batch, hipStream_t s,
-                   const float4 *pq_pre = nullptr) {
-  int logl;
-  if (overlap_save) {
+                   const float4 *pq_pre = nullptr, int logl = 0) {
+  if (logl) {
+    // block fixed by a plan
+  } else if (overlap_save) {
     logl = os_block_log(hlen);
   } else {
     logl = kRealMinLog;
@@ -1120,8 +1283,6 @@ vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, i
     VS_CASE(12, 0)
 #undef VS_CASE
     case 13:
-      if (g_conv_real == 2)
-        return run_real_t<13, 16>(correlate, h, hlen, hs, nfilt, a, nblocks, pq_pre, s);
       return run_real_t<13, 32>(correlate, h, hlen, hs, nfilt, a, nblocks, pq_pre, s);
     case 14:
       return run_real_t<14, 0>(correlate, h, hlen, hs, nfilt, a, nblocks, pq_pre, s);
@@ -1130,29 +1291,91 @@ vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, i
   return VS_ERR_UNSUPPORTED;
 }
 
-// Filters too long for one overlap-save block: partitions of kPartTaps taps,
-// each an overlap-save pass whose outputs are added at the partition's
-// offset, y = sum_p (x * h_p)[n - p kPartTaps].  Correlation partitions the
-// reversed filter (partition p of it is h[hlen - p P - len_p, ...) reversed).
-vs_status run_partitioned(int correlate, const float *x, int xlen, int64_t xs,
-                          const float *h, int hlen, int64_t hs, float *y, int64_t ys,
-                          int batch, hipStream_t s) {
-  const int ylen = xlen + hlen - 1;
-  // the first pass writes [0, xlen + kPartTaps - 1); later passes add into
-  // the rest of the row, which starts at zero
-  const int head = xlen + std::min(kPartTaps, hlen) - 1;
-  if (head < ylen)
-    VS_HIP(hipMemset2DAsync(y + head, static_cast<size_t>(ys) * sizeof(float), 0,
-                            static_cast<size_t>(ylen - head) * sizeof(float),
-                            static_cast<size_t>(batch), s));
-  for (int p0 = 0, part = 0; p0 < hlen; p0 += kPartTaps, part++) {
-    const int len = std::min(kPartTaps, hlen - p0);
-    const float *hp = correlate ? h + (hlen - p0 - len) : h + p0;
-    log(2, "vs_conv1d: partition %d taps [%d, %d)", part, p0, p0 + len);
-    VS_TRY(run_real(correlate, true, x, xlen, xs, hp, len, hs, y + p0, ys, xlen + len - 1,
-                    ylen - p0, part > 0, batch, s));
+// Filters too long for one overlap-save block: uniformly partitioned
+// overlap-save (fdl_*_kernel above).  Blocks of L = 2^g_fdl_log samples, B =
+// L / 2 taps per partition.  `pq_pre`: the partitions' P / Q tables when a
+// plan holds them.  Signals go through in groups whose spectra (Z and Y:
+// 16 bytes per sample and per output) fit kFdlScratch.
+constexpr size_t kFdlScratch = static_cast<size_t>(6) << 30;
+
+template <int LOGM, int EP>
+vs_status run_fdl_t(int correlate, const float *x, int xlen, int64_t xs, const float *h,
+                    int hlen, int64_t hs, float *y, int64_t ys, int ylen, int batch,
+                    hipStream_t s, const float4 *pq_pre) {
+  using PL = Plan<LOGM, EP>;
+  constexpr int M = PL::N, B = M;
+  const int parts = (hlen + B - 1) / B;
+  const int nblk = (ylen + B - 1) / B;
+  // source block b holds x[(b - 1) B, (b + 1) B): all zero from (xlen - 1) / B + 2 on
+  const int nsrc = std::min((xlen - 1) / B + 2, nblk);
+  const int nfilt = hs ? batch : 1;
+  vs_status st;
+  const float2 *tw = fft::twiddles(LOGM, &st);
+  if (!tw) return st;
+  DeviceBuffer pq;
+  const float4 *PQ = pq_pre;
+  if (!PQ) {
+    VS_TRY(pq.alloc(sizeof(float4) * M * static_cast<size_t>(parts) * nfilt, s));
+    VS_TRY(launch_real_filter<LOGM>(correlate, h, hlen, hs, nfilt, pq.as<float4>(), s, B));
+    PQ = pq.as<float4>();
+  }
+  const size_t per_sig = (static_cast<size_t>(nsrc) + nblk) * M * sizeof(float2);
+  const int group = static_cast<int>(
+      std::max<size_t>(1, std::min<size_t>({static_cast<size_t>(batch), kFdlScratch / per_sig,
+                                            static_cast<size_t>(kMaxGridY)})));
+  DeviceBuffer zy;
+  VS_TRY(zy.alloc(per_sig * group, s));
+  float2 *Z = zy.as<float2>(), *Y = Z + static_cast<size_t>(group) * nsrc * M;
+  const bool buf = g_conv_buf && xlen < (1 << 29) && ylen < (1 << 29);
+  log(2, "vs_conv1d: partitioned overlap-save, L=%d, %d partitions, %d + %d blocks, groups of %d",
+      2 * M, parts, nsrc, nblk, group);
+  for (int b0 = 0; b0 < batch; b0 += group) {
+    const int nb = std::min(group, batch - b0);
+    RealArgs a{};
+    a.x = x + static_cast<int64_t>(b0) * xs;
+    a.xs = xs;
+    a.xlen = xlen;
+    a.y = y + static_cast<int64_t>(b0) * ys;
+    a.ys = ys;
+    a.ylen = ylen;
+    a.yroom = ylen;
+    a.pre = B;
+    a.step = B;
+    a.nblk = nblk;
+    const dim3 gf(static_cast<unsigned>(nsrc), static_cast<unsigned>(nb));
+    const dim3 gi(static_cast<unsigned>(nblk), static_cast<unsigned>(nb));
+    if (buf)
+      hipLaunchKernelGGL((fdl_forward_kernel<LOGM, EP, true>), gf, dim3(PL::TPS), 0, s, a, Z, tw);
+    else
+      hipLaunchKernelGGL((fdl_forward_kernel<LOGM, EP, false>), gf, dim3(PL::TPS), 0, s, a, Z, tw);
+    FdlMac m{Z, PQ + (hs ? static_cast<size_t>(b0) * parts * M : 0), Y, nsrc, nblk, parts, M,
+             hs != 0};
+    hipLaunchKernelGGL(fdl_mac_kernel,
+                       dim3((M / 2 + 1 + 255) / 256,
+                            static_cast<unsigned>((nblk + kFdlTile - 1) / kFdlTile),
+                            static_cast<unsigned>(nb)),
+                       dim3(256), 0, s, m);
+    if (buf)
+      hipLaunchKernelGGL((fdl_inverse_kernel<LOGM, EP, true>), gi, dim3(PL::TPS), 0, s, a, Y, tw);
+    else
+      hipLaunchKernelGGL((fdl_inverse_kernel<LOGM, EP, false>), gi, dim3(PL::TPS), 0, s, a, Y, tw);
+    VS_HIP(hipGetLastError());
   }
   return VS_OK;
+}
+
+// log2 of the block of the partitioned path (vs_tune_set("fdl_block_log")).
+thread_local int g_fdl_log = 14;
+
+int fdl_part_taps() { return 1 << (g_fdl_log - 1); }
+
+vs_status run_partitioned(int correlate, const float *x, int xlen, int64_t xs,
+                          const float *h, int hlen, int64_t hs, float *y, int64_t ys, int ylen,
+                          int batch, hipStream_t s, const float4 *pq_pre = nullptr,
+                          int logl = 0) {
+  if ((logl ? logl : g_fdl_log) == 13)
+    return run_fdl_t<12, 0>(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s, pq_pre);
+  return run_fdl_t<13, 32>(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s, pq_pre);
 }
 
 vs_status run_fft_large(int correlate, const float *x, int xlen, int64_t xs,
@@ -1206,6 +1429,7 @@ vs_status run_fft_large(int correlate, const float *x, int xlen, int64_t xs,
 namespace vs {
 namespace wav {
 bool tune(const char *key, int value);
+void tune_reset();
 }
 }  // namespace vs
 
@@ -1299,7 +1523,7 @@ __attribute__((visibility("default"))) int vs_conv_occupancy(int which) {
 }
 #endif
 
-int vs_conv1d_select(int xlen, int hlen, int batch) {
+int vs_conv1d_select(int64_t xlen, int hlen, int batch) {
   return conv::select(xlen, hlen, batch);
 }
 
@@ -1310,7 +1534,9 @@ int vs_conv1d_os_block(int hlen) { return 1 << conv::os_block_log(hlen); }
 struct vs_conv_plan {
   int algo, correlate, xlen, hlen, nfilt;
   bool overlap_save;  // real plans: overlap-save blocks vs one block
-  float4 *pq;         // real plans: nfilt x 2^(logl-1) P / Q entries
+  int logl;           // real plans: block of 2^logl samples
+  int parts;          // > 0: partitioned overlap-save, filter partitions
+  float4 *pq;         // real plans: nfilt x max(parts, 1) x 2^(logl-1) P / Q entries
   float *h;           // other plans: nfilt x hlen taps
 };
 
@@ -1330,11 +1556,17 @@ vs_status vs_conv1d_plan_create(int algo, int correlate, int xlen, const float *
   VS_REQUIRE(algo >= VS_CONV_DIRECT && algo <= VS_CONV_OVERLAP_SAVE,
              "vs_conv1d_plan_create: unknown algorithm %d", algo);
   // The real-block path vs_conv1d would take for this shape, if any
-  int logl = 0;
+  int logl = 0, parts = 0;
   bool os = false;
   if (algo == VS_CONV_OVERLAP_SAVE) {
     const int l = conv::os_block_log(hlen);
-    if ((1 << l) > hlen - 1 + 16 && conv::use_real(l)) logl = l, os = true;
+    if (conv::os_single_block(hlen)) {
+      if (conv::use_real(l)) logl = l, os = true;
+    } else {  // partitioned: one P / Q table per partition
+      logl = conv::g_fdl_log == 13 ? 13 : 14;
+      parts = (hlen + (1 << (logl - 1)) - 1) >> (logl - 1);
+      os = true;
+    }
   } else if (algo == VS_CONV_FFT) {
     int lm = 1;
     while ((1LL << lm) < ylen) lm++;
@@ -1343,10 +1575,11 @@ vs_status vs_conv1d_plan_create(int algo, int correlate, int xlen, const float *
       while ((1LL << logl) < ylen) logl++;
     }
   }
-  auto *p = new vs_conv_plan{algo, correlate, xlen, hlen, nfilt, os, nullptr, nullptr};
+  auto *p = new vs_conv_plan{algo, correlate, xlen, hlen, nfilt, os, logl, parts, nullptr, nullptr};
   vs_status st = VS_OK;
   if (logl) {
-    const size_t n = (static_cast<size_t>(1) << (logl - 1)) * nfilt;
+    const size_t n = (static_cast<size_t>(1) << (logl - 1)) * nfilt * std::max(parts, 1);
+    const int part_taps = parts ? 1 << (logl - 1) : 0;
     if (hipMalloc(&p->pq, n * sizeof(float4)) != hipSuccess) {
       (void)hipGetLastError();
       st = VS_ERR_ALLOC;
@@ -1355,7 +1588,8 @@ vs_status vs_conv1d_plan_create(int algo, int correlate, int xlen, const float *
       switch (logl - 1) {
 #define VS_CASE(LG)                                                                           \
   case LG:                                                                                    \
-    st = conv::launch_real_filter<LG>(correlate, h, hlen, nfilt > 1 ? hs : 0, nfilt, p->pq, s); \
+    st = conv::launch_real_filter<LG>(correlate, h, hlen, nfilt > 1 ? hs : 0, nfilt, p->pq, s, \
+                                      part_taps);                                              \
     break;
         VS_CASE(6) VS_CASE(7) VS_CASE(8) VS_CASE(9) VS_CASE(10) VS_CASE(11) VS_CASE(12)
         VS_CASE(13) VS_CASE(14)
@@ -1402,15 +1636,20 @@ vs_status vs_conv1d_plan_execute(const vs_conv_plan *p, const float *x, int64_t 
   if (!p->pq)
     return vs_conv1d(p->algo, p->correlate, x, p->xlen, xs, p->h, p->hlen,
                      p->nfilt > 1 ? p->hlen : 0, y, ys, batch, stream);
-  if (batch > kMaxGridY) {
+  if (batch > kMaxGridY && !p->parts) {
     VS_REQUIRE(p->nfilt == 1, "vs_conv1d_plan_execute: per-signal batch > %lld", kMaxGridY);
     return batch_chunks(batch, [&](long long b0, int nb) {
       return vs_conv1d_plan_execute(p, x + b0 * xs, xs, y + b0 * ys, ys, nb, stream);
     });
   }
   // h is not read when the spectra are precomputed; hs only flags per-signal P / Q
+  if (p->parts)
+    return conv::run_partitioned(p->correlate, x, p->xlen, xs, nullptr, p->hlen,
+                                 p->nfilt > 1 ? p->hlen : 0, y, ys, ylen, batch, s, p->pq,
+                                 p->logl);
   return conv::run_real(p->correlate, p->overlap_save, x, p->xlen, xs, nullptr, p->hlen,
-                        p->nfilt > 1 ? p->hlen : 0, y, ys, ylen, ylen, 0, batch, s, p->pq);
+                        p->nfilt > 1 ? p->hlen : 0, y, ys, ylen, ylen, 0, batch, s, p->pq,
+                        p->logl);
 }
 
 vs_status vs_conv1d_plan_info(const vs_conv_plan *p, int *algo, int *precomputed) {
@@ -1444,7 +1683,7 @@ vs_status vs_tune_set(const char *key, int value) {
     return VS_OK;
   }
   if (std::strcmp(key, "conv_real") == 0) {
-    VS_REQUIRE(value >= 0 && value <= 2, "conv_real must be 0, 1 or 2");
+    VS_REQUIRE(value == 0 || value == 1, "conv_real must be 0 or 1");
     conv::g_conv_real = value;
     return VS_OK;
   }
@@ -1456,61 +1695,128 @@ vs_status vs_tune_set(const char *key, int value) {
     conv::g_conv_real_all = value != 0;
     return VS_OK;
   }
+  if (std::strcmp(key, "conv_piece_log") == 0) {
+    VS_REQUIRE(value >= 10 && value <= 28, "conv_piece_log must be 10..28");
+    conv::g_piece_log = value;
+    return VS_OK;
+  }
+  if (std::strcmp(key, "fdl_block_log") == 0) {
+    VS_REQUIRE(value == 13 || value == 14, "fdl_block_log must be 13 or 14");
+    conv::g_fdl_log = value;
+    return VS_OK;
+  }
   if (wav::tune(key, value)) return VS_OK;
   set_error("vs_tune_set: unknown key '%s'", key);
   return VS_ERR_INVALID;
 }
 
-vs_status vs_conv1d(int algo, int correlate, const float *x, int xlen,
+void vs_tune_reset(void) {
+  conv::g_os_log_max = fft::kMaxLdsLog + 1;
+  conv::g_os_extra = 0;
+  conv::g_conv_fused4 = 1;
+  conv::g_conv_buf = 1;
+  conv::g_conv_real = 1;
+  conv::g_conv_real_all = 0;
+  conv::g_fdl_log = 14;
+  conv::g_piece_log = 28;
+  wav::tune_reset();
+}
+
+}  // extern "C"
+
+namespace vs {
+namespace conv {
+
+// One launch sequence: lengths within the kernels' 32-bit indexing, the
+// first `ylen` (<= xlen + hlen - 1) outputs of every row written.
+vs_status dispatch(int algo, int correlate, const float *x, int xlen, int64_t xs,
+                   const float *h, int hlen, int64_t hs, float *y, int64_t ys, int ylen,
+                   int batch, hipStream_t s) {
+  const long long full = static_cast<long long>(xlen) + hlen - 1;
+  log(2, "vs_conv1d: x=%d h=%d batch=%d algo=%d outputs=%d", xlen, hlen, batch, algo, ylen);
+  int lm = 1;
+  while ((1LL << lm) < full) lm++;
+  switch (algo) {
+    case VS_CONV_DIRECT:
+      return run_direct(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s);
+    case VS_CONV_OVERLAP_SAVE:
+      if (os_single_block(hlen)) {
+        if (use_real(os_block_log(hlen)))
+          return run_real(correlate, true, x, xlen, xs, h, hlen, hs, y, ys, ylen, ylen, 0, batch,
+                          s);
+        return run_block(correlate, true, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s);
+      }
+      log(1, "vs_conv1d: filter %d longer than an overlap-save block: %d partitions", hlen,
+          (hlen + fdl_part_taps() - 1) / fdl_part_taps());
+      return run_partitioned(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s);
+    case VS_CONV_FFT:
+      if (lm <= fft::kMaxLdsLog || (lm == fft::kMaxLdsLog + 1 && use_real(lm))) {
+        if (use_real(lm))
+          return run_real(correlate, false, x, xlen, xs, h, hlen, hs, y, ys, ylen, ylen, 0, batch,
+                          s);
+        return run_block(correlate, false, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s);
+      }
+      if (lm <= fft::kMaxLog && hs == 0 && ylen == full)
+        return run_fft_large(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+      // beyond the largest transform, one filter per signal, or a piece of a
+      // longer row: overlap-save (partitioned when the filter needs it)
+      log(1, "vs_conv1d: FFT of 2^%d%s: overlap-save", lm, hs ? " with per-signal filters" : "");
+      return dispatch(VS_CONV_OVERLAP_SAVE, correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen,
+                      batch, s);
+  }
+  set_error("vs_conv1d: unknown algorithm %d", algo);
+  return VS_ERR_INVALID;
+}
+
+}  // namespace conv
+}  // namespace vs
+
+extern "C" {
+
+vs_status vs_conv1d(int algo, int correlate, const float *x, int64_t xlen,
                     int64_t xs, const float *h, int hlen, int64_t hs, float *y,
                     int64_t ys, int batch, vs_stream_t stream) {
   VS_REQUIRE(x && h && y, "vs_conv1d: null pointer");
   VS_REQUIRE(xlen > 0 && hlen > 0 && batch >= 0, "vs_conv1d: empty input");
+  VS_REQUIRE(hlen < (1 << 30), "vs_conv1d: filter of %d taps too long", hlen);
   const long long ylen = static_cast<long long>(xlen) + hlen - 1;
-  VS_REQUIRE(ylen < (1LL << 31), "vs_conv1d: output too long");
   VS_REQUIRE(batch <= 1 || (xs >= xlen && ys >= ylen),
              "vs_conv1d: row strides smaller than the rows");
   VS_REQUIRE(hs == 0 || hs >= hlen, "vs_conv1d: filter stride < filter length");
   if (batch == 0) return VS_OK;
   auto s = static_cast<hipStream_t>(stream);
   if (algo == VS_CONV_AUTO) algo = conv::select(xlen, hlen, batch);
+  VS_REQUIRE(algo >= VS_CONV_DIRECT && algo <= VS_CONV_OVERLAP_SAVE,
+             "vs_conv1d: unknown algorithm %d", algo);
   if (batch > kMaxGridY)
     return batch_chunks(batch, [&](long long b0, int nb) {
       return vs_conv1d(algo, correlate, x + b0 * xs, xlen, xs, h + b0 * hs, hlen, hs,
                        y + b0 * ys, ys, nb, stream);
     });
-  log(2, "vs_conv1d: x=%d h=%d batch=%d algo=%d", xlen, hlen, batch, algo);
-  int lm = 1;
-  while ((1LL << lm) < ylen) lm++;
-  switch (algo) {
-    case VS_CONV_DIRECT:
-      return conv::run_direct(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
-    case VS_CONV_OVERLAP_SAVE:
-      if ((1 << conv::os_block_log(hlen)) > hlen - 1 + 16) {
-        if (conv::use_real(conv::os_block_log(hlen)))
-          return conv::run_real(correlate, true, x, xlen, xs, h, hlen, hs, y, ys,
-                                static_cast<int>(ylen), static_cast<int>(ylen), 0, batch, s);
-        return conv::run_block(correlate, true, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
-      }
-      log(1, "vs_conv1d: filter %d longer than an overlap-save block: %d partitions", hlen,
-          (hlen + conv::kPartTaps - 1) / conv::kPartTaps);
-      return conv::run_partitioned(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
-    case VS_CONV_FFT:
-      if (lm <= fft::kMaxLdsLog || (lm == fft::kMaxLdsLog + 1 && conv::use_real(lm))) {
-        if (conv::use_real(lm))
-          return conv::run_real(correlate, false, x, xlen, xs, h, hlen, hs, y, ys,
-                                static_cast<int>(ylen), static_cast<int>(ylen), 0, batch, s);
-        return conv::run_block(correlate, false, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
-      }
-      if (lm <= fft::kMaxLog && hs == 0)
-        return conv::run_fft_large(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
-      // beyond the largest transform, or one filter per signal: partitions
-      log(1, "vs_conv1d: FFT of 2^%d%s: partitioned overlap-save", lm,
-          hs ? " with per-signal filters" : "");
-      return conv::run_partitioned(correlate, x, xlen, xs, h, hlen, hs, y, ys, batch, s);
+  if (ylen <= conv::max_call_out())
+    return conv::dispatch(algo, correlate, x, static_cast<int>(xlen), xs, h, hlen, hs, y, ys,
+                          static_cast<int>(ylen), batch, s);
+  // Long rows: pieces of 2^28 outputs, each the convolution of its x
+  // samples and the hlen - 1 before them.  A piece writes from the first
+  // output its x range produces -- the `skip` outputs before its own range
+  // lack their history -- and stops at the end of its range; the pieces run
+  // last to first, so the piece that owns those `skip` outputs overwrites
+  // them afterwards (same stream).
+  if (algo == VS_CONV_FFT) algo = VS_CONV_OVERLAP_SAVE;
+  const long long piece = conv::piece_out();
+  const long long pieces = (ylen + piece - 1) / piece;
+  log(1, "vs_conv1d: x=%lld in %lld pieces of %lld outputs", static_cast<long long>(xlen), pieces,
+      piece);
+  for (long long c = pieces - 1; c >= 0; c--) {
+    const long long o0 = c * piece;
+    const long long olen = std::min(piece, ylen - o0);
+    const long long x0 = std::max<long long>(0, o0 - (hlen - 1));
+    const long long x1 = std::min<long long>(xlen, o0 + olen);
+    const long long skip = o0 - x0;
+    VS_TRY(conv::dispatch(algo, correlate, x + x0, static_cast<int>(x1 - x0), xs, h, hlen, hs,
+                          y + x0, ys, static_cast<int>(skip + olen), batch, s));
   }
-  set_error("vs_conv1d: unknown algorithm %d", algo);
-  return VS_ERR_INVALID;
+  return VS_OK;
 }
 
 }  // extern "C"

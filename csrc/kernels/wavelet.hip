@@ -551,13 +551,13 @@ vs_status launch_swt_tiled(const Taps &t, int ext, int levels, const float *src,
 // Tuning knobs (vs_tune_set): "swt_fused" 0 = round-1 multi4 kernel,
 // 1 (default) = fused-extension kernel; "swt_nt" 1 (default) = non-temporal
 // hi stores (+3 % on db8 x 8 levels: the hi rows are never re-read here).
-int g_swt_fused = 1;
-int g_swt_nt = 1;
+thread_local int g_swt_fused = 1;
+thread_local int g_swt_nt = 1;
 // "dwt_vec" 1 (default) = vectorised pyramid kernel (dwt_multi4_kernel),
 // 0 = the scalar round-1 kernel.
-int g_dwt_vec = 1;
+thread_local int g_dwt_vec = 1;
 // "dwt_threads": workgroup size of the vectorised pyramid (0 = auto).
-int g_dwt_threads = 0;
+thread_local int g_dwt_threads = 0;
 
 template <int ORDER>
 vs_status launch_swt_multi4(const Taps &t, int ext, int levels, const float *src, int len,
@@ -829,6 +829,13 @@ bool tune(const char *key, int value) {
     return true;
   }
   return false;
+}
+
+void tune_reset() {
+  g_swt_fused = 1;
+  g_swt_nt = 1;
+  g_dwt_vec = 1;
+  g_dwt_threads = 0;
 }
 
 }  // namespace wav

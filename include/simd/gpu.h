@@ -247,12 +247,12 @@ typedef enum {
 /// Batched full linear convolution (correlate=0) or cross-correlation
 /// (correlate=1): y[b] (length x_len + h_len - 1, row stride y_stride) of
 /// x[b] (stride x_stride) with h[b] (stride h_stride; 0 = one shared filter).
-vs_status vs_conv1d(int algo, int correlate, const float *x, int x_len,
+vs_status vs_conv1d(int algo, int correlate, const float *x, int64_t x_len,
                     int64_t x_stride, const float *h, int h_len,
                     int64_t h_stride, float *y, int64_t y_stride, int batch,
                     vs_stream_t stream);
 /// Algorithm VS_CONV_AUTO resolves to for this shape.
-int vs_conv1d_select(int x_len, int h_len, int batch);
+int vs_conv1d_select(int64_t x_len, int h_len, int batch);
 /// Overlap-save block length the library uses for filter length h_len.
 int vs_conv1d_os_block(int h_len);
 
@@ -278,7 +278,11 @@ vs_status vs_conv1d_plan_info(const vs_conv_plan *plan, int *algo, int *precompu
 void vs_conv1d_plan_destroy(vs_conv_plan *plan);
 /// Tuning knobs for measurements ("os_block_log_max": cap of the
 /// overlap-save block, log2).
+/// The knobs are per thread: a call changes what later calls of the same
+/// thread do, never another thread's; plans keep what they were created with.
 vs_status vs_tune_set(const char *key, int value);
+/// Restores every knob of the calling thread to its default.
+void vs_tune_reset(void);
 
 /* -------------------------------------------------------------- wavelets */
 /// Batched single-level decimated DWT: hi/lo rows of len/2 (stride

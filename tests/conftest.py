@@ -34,3 +34,14 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _default_tuning_knobs():
+    """Every test starts from and leaves behind the default tuning knobs
+    (vs_tune_set is per thread; a test that fails between a set and its
+    restore must not leak into the next test)."""
+    yield
+    from veles.simd_amd import _lib
+    if _lib.available():
+        _lib.lib().vs_tune_reset()

@@ -1,11 +1,12 @@
 """Every device convolution path against an fp64 reference.
 
 Covers the real-block overlap-save kernel (conv.hip real_conv_kernel) and the
-pair kernel it replaced (tuning knob conv_real = 0), both point-per-thread
-plans of the 8192-point block (conv_real = 2), odd signal / filter lengths
-(odd block starts, half-valid 8-byte edges), per-signal filters, the
-partitioned path for filters longer than one overlap-save block, and padded
-lengths beyond the single-workgroup transform (four-step, up to 2^24).
+pair kernel it replaced (tuning knob conv_real = 0), odd signal / filter
+lengths (odd block starts, half-valid 8-byte edges), per-signal filters, the
+uniformly partitioned path for filters longer than one overlap-save block,
+rows cut into pieces (the path of rows of 2^29 outputs or more, exercised on
+short rows through the conv_piece_log knob), and padded lengths beyond the
+single-workgroup transform (four-step, up to 2^24).
 Reference behaviour: /root/reference/src/convolve.c:116-121 (any h < x/2 runs
 overlap-save), :237-244 (FFT has no size cap).
 """
@@ -36,8 +37,7 @@ def _knob(name, value, default):
 
 @contextlib.contextmanager
 def _kernel(real):
-    """real: 0 pair kernel, 1 real-block kernel at every block size,
-    2 real-block kernel with the 16-point plan at M = 8192."""
+    """real: 0 pair kernel, 1 real-block kernel at every block size."""
     with _knob("conv_real", real, 1), _knob("conv_real_all", int(real == 1), 0):
         yield
 
@@ -59,7 +59,7 @@ def _check(xlen, hlen, batch, algo, corr, per_signal=False, seed=0, rel=2e-6):
         assert err <= tol + 1e-4, (xlen, hlen, b, algo, corr, err, tol)
 
 
-@pytest.mark.parametrize("real", [0, 1, 2])
+@pytest.mark.parametrize("real", [0, 1])
 @pytest.mark.parametrize("xlen,hlen,batch", [
     (1 << 16, 4096, 3),      # L = 16384 (M = 8192), pre odd
     (100003, 4095, 2),       # odd x, pre even
@@ -190,16 +190,126 @@ def test_partitioned_beyond_32768_block():
     _check(200000, 40000, 1, "overlap_save", True)
 
 
+@pytest.mark.parametrize("block_log", [14, 13])
+@pytest.mark.parametrize("xlen,hlen,batch,per_signal", [
+    (1 << 18, 65536, 2, False),    # 8 partitions of 8192 taps
+    (100003, 200000, 2, False),    # filter longer than the signal, ragged last partition
+    (1 << 17, 70001, 3, True),     # one filter per signal
+    (40000, 32769, 1, False),      # just past the largest single block
+    (300001, 49153, 2, False),     # odd lengths, 6 partitions + 1 tap
+])
+@pytest.mark.parametrize("corr", [False, True])
+def test_uniformly_partitioned_overlap_save(block_log, xlen, hlen, batch, per_signal, corr):
+    """Frequency-domain delay line (conv.hip fdl_*_kernel): every x block
+    transformed once, partition spectra accumulated per output block, one
+    inverse per block; both block sizes (L = 16384 default, 8192)."""
+    with _knob("fdl_block_log", block_log, 14):
+        _check(xlen, hlen, batch, "overlap_save", corr, per_signal=per_signal)
+
+
+def test_partitioned_many_output_tiles():
+    """More output blocks than one accumulation tile (16) and more than four
+    partitions: every (tile, partition group) edge of fdl_mac_kernel."""
+    _check(8192 * 37 + 5, 8192 * 5 + 77, 2, "overlap_save", False)
+    with _knob("fdl_block_log", 13, 14):
+        _check(4096 * 41 + 3, 4096 * 9 + 1, 1, "overlap_save", True)
+
+
+def test_partitioned_plan_matches_call():
+    """A plan of a partitioned shape holds the partitions' P / Q tables and
+    gives the per-call result bit for bit."""
+    import torch
+    from veles.simd_amd import ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 150000, generator=g).cuda()
+    for h in (torch.randn(50000, generator=g).cuda(), torch.randn(3, 40001, generator=g).cuda()):
+        plan = ops.Conv1dPlan(h, x.shape[1], algorithm="overlap_save")
+        assert plan.precomputed
+        y = plan(x)
+        want = ops.conv1d(x, h, algorithm="overlap_save")
+        assert torch.equal(y, want)
+
+
+@pytest.mark.parametrize("algo,hlen,real", [
+    ("direct", 4, 1), ("direct", 29, 1), ("direct", 700, 1),
+    ("overlap_save", 1000, 1), ("overlap_save", 4096, 1), ("overlap_save", 1000, 0),
+    ("overlap_save", 40000, 1), ("auto", 3000, 1), ("fft", 515, 1)])
+@pytest.mark.parametrize("corr", [False, True])
+def test_rows_cut_into_pieces(algo, hlen, real, corr):
+    """Rows of 2^29 outputs or more are cut into pieces of 2^28 outputs run
+    last to first (vs_conv1d); conv_piece_log = 14 runs the same code on a
+    row of ~100k samples: 7 pieces, filters shorter and longer than a piece,
+    every algorithm, shared and per-signal filters."""
+    with _knob("conv_piece_log", 14, 28), _kernel(real):
+        _check(100003, hlen, 2, algo, corr)
+        _check(65536 - hlen + 1, hlen, 1, algo, corr)   # outputs end on a piece edge
+        if algo != "fft":
+            _check(70001, hlen, 2, algo, corr, per_signal=True)
+
+
+def _window_ref(x, h, lo, hi, corr):
+    """fp64 outputs [lo, hi) of conv(x, h) from the x samples they touch."""
+    from scipy.signal import fftconvolve
+    m = h.numel()
+    a = max(0, lo - (m - 1))
+    b = min(x.numel(), hi)
+    xw = x[a:b].cpu().double().numpy()
+    hw = h.cpu().double().numpy()
+    full = fftconvolve(xw, hw[::-1] if corr else hw)   # output n of the window = a + n
+    return full[lo - a:hi - a]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n,hlen,algo", [((1 << 32) + 17, 4096, "auto"),
+                                         ((1 << 31) + 5, 4, "auto"),
+                                         ((1 << 29) + 1001, 40000, "overlap_save")])
+def test_rows_beyond_2p31(n, hlen, algo):
+    """Signals of 2^31 samples and more on one GPU (reference
+    inc/simd/convolve.h:100-111 takes size_t lengths): fp64 spot checks at the
+    start, around every piece edge and at the end."""
+    import torch
+    from veles.simd_amd import ops
+    x = torch.empty(n, device="cuda")
+    step = 1 << 28
+    g = torch.Generator(device="cuda").manual_seed(n % 1000)
+    for a in range(0, n, step):
+        x[a:a + step].normal_(generator=g)
+    h = torch.randn(hlen, device="cuda")
+    y = ops.conv1d(x, h, algorithm=algo)
+    ylen = n + hlen - 1
+    assert y.shape == (ylen,)
+    spots = [(0, 300), (ylen - 300, ylen)]
+    for e in range(step, ylen, step):
+        spots.append((e - 150, e + 150))
+    tol = 2e-6 * np.sqrt(hlen) * 30 * 25
+    for lo, hi in spots:
+        ref = _window_ref(x, h, lo, hi, False)
+        got = y[lo:hi].cpu().double().numpy()
+        assert np.abs(got - ref).max() <= tol, (lo, hi, np.abs(got - ref).max())
+    del y
+    # correlation of the same row: only the piece edges differ in kind
+    y = ops.conv1d(x, h, algorithm=algo, correlate=True)
+    for lo, hi in spots[:3]:
+        ref = _window_ref(x, h, lo, hi, True)
+        got = y[lo:hi].cpu().double().numpy()
+        assert np.abs(got - ref).max() <= tol, (lo, hi)
+
+
 def test_select_long_filter_overlap_save():
-    """Filters whose L = 32768 block is >= 20 % useful run overlap-save
-    (h = 20000: 144 vs 73 Gsamples/s for the fused four-step FFT); shorter blocks
-    fall back to the FFT (profiles/r2/conv/conv_long.log)."""
+    """Filters whose L = 32768 block is >= 28 % useful run single-block
+    overlap-save (h = 20000: 144 vs 73 Gsamples/s for the fused four-step
+    FFT); longer ones the uniformly partitioned path up to 12 partitions of
+    8192 taps (h = 65536: 89 vs 70), then the FFT (profiles/r3/conv/fdl.md)."""
     from veles.simd_amd import _lib
     lib = _lib.lib()
     assert lib.vs_conv1d_select(1 << 20, 20000, 64) == 3
-    assert lib.vs_conv1d_select(1 << 20, 30000, 64) == 2
+    assert lib.vs_conv1d_select(1 << 20, 30000, 64) == 3
+    assert lib.vs_conv1d_select(1 << 20, 98304, 64) == 3
+    assert lib.vs_conv1d_select(1 << 20, 200000, 64) == 2
+    assert lib.vs_conv1d_select(1 << 27, 200000, 1) == 3   # beyond the largest transform
     _check(200000, 20000, 2, "auto", False)
     _check(200000, 20000, 1, "auto", True)
+    _check(200000, 30000, 2, "auto", False)
 
 
 @pytest.mark.parametrize("xlen,hlen,batch", [(300000, 40000, 3), (100003, 60000, 2),

@@ -84,15 +84,16 @@ _SIGNATURES = {
     "vs_fft_c2c": (_i, [_vp, _vp, _i, _i, _i, _vp]),
     "vs_fft_r2c": (_i, [_vp, _vp, _i, _i, _vp]),
     "vs_fft_c2r": (_i, [_vp, _vp, _i, _i, _vp]),
-    "vs_conv1d": (_i, [_i, _i, _vp, _i, _i64, _vp, _i, _i64, _vp, _i64, _i,
+    "vs_conv1d": (_i, [_i, _i, _vp, _i64, _i64, _vp, _i, _i64, _vp, _i64, _i,
                        _vp]),
-    "vs_conv1d_select": (_i, [_i, _i, _i]),
+    "vs_conv1d_select": (_i, [_i64, _i, _i]),
     "vs_conv1d_plan_create": (_i, [_i, _i, _i, _vp, _i, _i64, _i, ctypes.POINTER(_vp), _vp]),
     "vs_conv1d_plan_execute": (_i, [_vp, _vp, _i64, _vp, _i64, _i, _vp]),
     "vs_conv1d_plan_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "vs_conv1d_plan_destroy": (None, [_vp]),
     "vs_conv1d_os_block": (_i, [_i]),
     "vs_tune_set": (_i, [ctypes.c_char_p, _i]),
+    "vs_tune_reset": (None, []),
     "vs_pow": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "vs_sincos": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "vs_dwt": (_i, [_i, _i, _i, _vp, _i, _i64, _vp, _vp, _i64, _i, _vp]),
