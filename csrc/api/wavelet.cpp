@@ -92,7 +92,7 @@ void wavelet_apply(WaveletType type, int order, ExtensionType ext,
     VS_TRY(h.status());
     VS_TRY(l.status());
     VS_TRY(x.status());
-    VS_TRY(vs_dwt(type, order, ext, x.dev<float>(), vs::api::checked_int("wavelet", length), 0,
+    VS_TRY(vs_dwt(type, order, ext, x.dev<float>(), static_cast<int64_t>(length), 0,
                   h.dev<float>(), l.dev<float>(), 0, 1, s));
     VS_TRY(h.finish());
     return l.finish();
@@ -124,7 +124,7 @@ void stationary_wavelet_apply(WaveletType type, int order, int level,
     VS_TRY(h.status());
     VS_TRY(l.status());
     VS_TRY(x.status());
-    VS_TRY(vs_swt(type, order, level, ext, x.dev<float>(), vs::api::checked_int("wavelet", length), 0,
+    VS_TRY(vs_swt(type, order, level, ext, x.dev<float>(), static_cast<int64_t>(length), 0,
                   h.dev<float>(), l.dev<float>(), 0, 1, s));
     VS_TRY(h.finish());
     return l.finish();

@@ -287,22 +287,22 @@ void vs_tune_reset(void);
 /* -------------------------------------------------------------- wavelets */
 /// Batched single-level decimated DWT: hi/lo rows of len/2 (stride
 /// out_stride) per input row (stride src_stride).
-vs_status vs_dwt(int type, int order, int ext, const float *src, int len,
+vs_status vs_dwt(int type, int order, int ext, const float *src, int64_t len,
                  int64_t src_stride, float *hi, float *lo, int64_t out_stride,
                  int batch, vs_stream_t stream);
 /// Batched single-level stationary DWT at `level` (full-length outputs).
 vs_status vs_swt(int type, int order, int level, int ext, const float *src,
-                 int len, int64_t src_stride, float *hi, float *lo,
+                 int64_t len, int64_t src_stride, float *hi, float *lo,
                  int64_t out_stride, int batch, vs_stream_t stream);
 /// Fused `levels`-level stationary DWT, level l fed by level l-1's lo:
 /// hi is [batch][levels][len], lo is [batch][len] (the last level's lo).
 vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
-                            const float *src, int len, float *hi, float *lo,
+                            const float *src, int64_t len, float *hi, float *lo,
                             int batch, vs_stream_t stream);
 /// Fused `levels`-level decimated DWT (Mallat pyramid); per row of out
 /// (length len): [hi_1 (len/2) | hi_2 (len/4) | ... | hi_L | lo_L].
 vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,
-                            const float *src, int len, float *out, int batch,
+                            const float *src, int64_t len, float *out, int batch,
                             vs_stream_t stream);
 /// Copies the float low-pass filter (order taps) into host memory `out`.
 vs_status vs_wavelet_filter(int type, int order, float *out);

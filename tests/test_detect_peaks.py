@@ -130,3 +130,26 @@ def test_matched_filter_batch_in_one_launch_sequence():
         keep = v > 12.0
         assert torch.equal(peaks[r][0], p[keep]) and torch.equal(peaks[r][1], v[keep])
     assert sum(p.numel() for p, _ in peaks) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_row_of_2p32_samples():
+    """A row of 2^32 + 3 samples (reference inc/simd/detect_peaks.h:61-62
+    takes size_t): positions come back as int64; spikes placed at the start,
+    around 2^31 and 2^32 and at the end are found exactly, with their values
+    and in order."""
+    import torch
+    from veles.simd_amd import ops
+    n = (1 << 32) + 3
+    x = torch.zeros(n, device="cuda")
+    want = [1, 4097, (1 << 31) - 1, 1 << 31, (1 << 31) + 7, (1 << 32) - 2, 1 << 32, n - 2]
+    vals = [float(i + 1) * (1 if i % 2 == 0 else -1) for i in range(len(want))]
+    x[torch.tensor(want, device="cuda")] = torch.tensor(vals, device="cuda")
+    # neighbours (2^31 - 1, 2^31): make both strict extrema of opposite sign
+    pos, val = ops.detect_peaks(x, "both")
+    assert pos.dtype == torch.int64
+    assert pos.cpu().tolist() == want
+    assert val.cpu().tolist() == vals
+    pos, val = ops.detect_peaks(x, "max")
+    assert pos.cpu().tolist() == [p for p, v in zip(want, vals) if v > 0]

@@ -349,3 +349,178 @@ def test_dwt_multilevel_vec(t, o, levels, n, e):
         cur = nxt
         off += m
     np.testing.assert_allclose(pyr[:, off:], cur, atol=5e-4)
+
+
+def _pyramid_ref(x, t, o, levels, e):
+    """Level-by-level host reference of the Mallat pyramid rows."""
+    b, n = x.shape
+    out = np.zeros((b, n), np.float32)
+    cur = x
+    off = 0
+    for _ in range(levels):
+        m = cur.shape[1] // 2
+        nxt = np.zeros((b, m), np.float32)
+        for r in range(b):
+            vhi, vlo = capi.wavelet_apply(t, o, e, cur[r], na=True)
+            out[r, off:off + m] = vhi
+            nxt[r] = vlo
+        cur = nxt
+        off += m
+    out[:, off:] = cur
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,o,levels,n", [
+    (D, 8, 8, 1 << 17),        # one tiled pass of 8 levels
+    (D, 8, 11, 1 << 16),       # two passes (8 + 3), second on a 256-sample band
+    (C, 30, 5, 3 * (1 << 14)),  # long filter: 4 levels + 1, ragged tile count
+    (S, 4, 3, 40000),          # last tile overlaps the one before
+    (D, 2, 12, 1 << 15),       # Haar, 12 levels down to 8 samples
+    (D, 16, 6, 20480),         # bands that stop being multiples of 4 (scalar levels)
+])
+@pytest.mark.parametrize("e", EXTS)
+def test_dwt_multilevel_long_tiled(t, o, levels, n, e):
+    """Pyramid of signals longer than the LDS kernel (vs_dwt_multilevel,
+    dwt_tiled_kernel): tiles with the multi-level support in LDS, hi bands
+    written straight into the pyramid row, against the level-by-level host
+    reference and the level-by-level device path (dwt_vec = 0)."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    b = 2
+    g = torch.Generator().manual_seed(o + levels + e)
+    x = torch.randn(b, n, generator=g)
+    xd = x.cuda()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for vec in (1, 0):
+        out = torch.full((b, n), float("nan"), device="cuda")
+        assert lib.vs_tune_set(b"dwt_vec", vec) == 0
+        st = lib.vs_dwt_multilevel(t, o, levels, e, ctypes.c_void_p(xd.data_ptr()), n,
+                                   ctypes.c_void_p(out.data_ptr()), b, s)
+        assert st == 0, lib.vs_last_error()
+        outs.append(out.cpu().numpy())
+    lib.vs_tune_set(b"dwt_vec", -1)
+    ref = _pyramid_ref(x.numpy(), t, o, levels, e)
+    scale = max(1.0, np.abs(ref).max())
+    np.testing.assert_allclose(outs[0], ref, atol=3e-5 * scale * levels)
+    np.testing.assert_allclose(outs[0], outs[1], atol=3e-5 * scale * levels)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,o", [(D, 8), (S, 16), (C, 6), (D, 76)])
+@pytest.mark.parametrize("n,off", [(512, 0), (1000, 0), (8192 + 24, 0), (40000, 0), (4098, 1)])
+@pytest.mark.parametrize("e", EXTS)
+def test_dwt_single_level_vectorised(t, o, n, off, e):
+    """Single decimated level (vs_dwt): the tiled kernel with compile-time
+    filter length and float4 loads / stores (orders without an
+    instantiation -- db76 -- and offset rows take the scalar paths), against
+    the host reference; rows with strides, hi / lo padded apart."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    b = 3
+    ss = n + 8
+    os_ = n // 2 + 4
+    g = torch.Generator().manual_seed(o + n + e)
+    xb = torch.randn(b * ss + off, generator=g)
+    xd = xb.cuda()
+    hi = torch.full((b * os_ + off,), 7.0, device="cuda")
+    lo = torch.full((b * os_ + off,), 7.0, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    st = lib.vs_dwt(t, o, e, ctypes.c_void_p(xd.data_ptr() + 4 * off), n, ss,
+                    ctypes.c_void_p(hi.data_ptr() + 4 * off), ctypes.c_void_p(lo.data_ptr() + 4 * off),
+                    os_, b, s)
+    assert st == 0, lib.vs_last_error()
+    hi = hi.cpu().numpy()[off:off + b * os_].reshape(b, os_)
+    lo = lo.cpu().numpy()[off:off + b * os_].reshape(b, os_)
+    x = xb.numpy()[off:off + b * ss].reshape(b, ss)[:, :n]
+    for r in range(b):
+        vhi, vlo = capi.wavelet_apply(t, o, e, x[r], na=True)
+        np.testing.assert_allclose(hi[r, :n // 2], vhi, atol=2e-4)
+        np.testing.assert_allclose(lo[r, :n // 2], vlo, atol=2e-4)
+    assert (hi[:, n // 2:] == 7.0).all() and (lo[:, n // 2:] == 7.0).all()
+
+
+def _window(x, a, b, n, e, halo):
+    """Host row x[a:b] followed by `halo` samples of what the transform sees
+    after it: the next samples, or the extension (e: 0 periodic, 1 mirror)
+    when the window ends at the end of the row."""
+    import torch
+    if b < n:
+        return x[a:b + halo].cpu().numpy()
+    tail = x[:halo] if e == 0 else x[n - halo:].flip(0)
+    return torch.cat([x[a:b], tail]).cpu().numpy()
+
+
+def _spots(n, w):
+    return [(0, w), ((n // 2) - w, (n // 2) + w), (n - 2 * w, n)]
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("e", [0, 1])
+def test_swt_and_dwt_rows_of_2p32(e):
+    """Rows of 2^32 samples (size_t lengths in the reference,
+    inc/simd/wavelet.h:61-100): stationary levels 1 and 2 (single-level and
+    fused tiled kernels, 64-bit positions) and a three-level pyramid.  Every
+    band is checked at its start, middle (around 2^31 of the input) and end
+    (extension) against the host reference run on windows of the band before
+    it, which the same checks validated."""
+    import ctypes
+    import torch
+    from veles.simd_amd import _lib
+    lib = _lib.lib()
+    n = 1 << 32
+    x = torch.empty(n, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for a in range(0, n, 1 << 28):
+        x[a:a + (1 << 28)].normal_(generator=g)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    vp = lambda t_: ctypes.c_void_p(t_.data_ptr())  # noqa: E731
+    W = 96
+
+    def check_swt(band_in, level, hi, lo, tol):
+        for a, b in _spots(n, W):
+            w = _window(band_in, a, b, n, e, 7 * (1 << (level - 1)) + 1)
+            vhi, vlo = capi.stationary_wavelet_apply(D, 8, level, 3, w, na=True)
+            np.testing.assert_allclose(hi[a:b].cpu().numpy(), vhi[:b - a], atol=tol)
+            np.testing.assert_allclose(lo[a:b].cpu().numpy(), vlo[:b - a], atol=tol)
+
+    hi1 = torch.empty(n, device="cuda")
+    lo1 = torch.empty(n, device="cuda")
+    assert lib.vs_swt(D, 8, 1, e, vp(x), n, n, vp(hi1), vp(lo1), n, 1, s) == 0, lib.vs_last_error()
+    check_swt(x, 1, hi1, lo1, 2e-5)
+    hi = torch.empty(2, n, device="cuda")
+    lo = torch.empty(n, device="cuda")
+    assert lib.vs_swt_multilevel(D, 8, 2, e, vp(x), n, vp(hi), vp(lo), 1, s) == 0, \
+        lib.vs_last_error()
+    for a, b in _spots(n, W):
+        np.testing.assert_allclose(hi[0, a:b].cpu().numpy(), hi1[a:b].cpu().numpy(), atol=1e-5)
+    check_swt(lo1, 2, hi[1], lo, 4e-5)
+    del hi, lo, hi1, lo1
+
+    out = torch.empty(n, device="cuda")
+    assert lib.vs_dwt_multilevel(D, 8, 3, e, vp(x), n, vp(out), 1, s) == 0, lib.vs_last_error()
+    cur, m, off = x, n, 0
+    for lvl in range(3):
+        half = m // 2
+        bh = torch.empty(half, device="cuda")
+        bl = torch.empty(half, device="cuda")
+        assert lib.vs_dwt(D, 8, e, vp(cur), m, m, vp(bh), vp(bl), half, 1, s) == 0, \
+            lib.vs_last_error()
+        for a, b in _spots(half, W):
+            w = _window(cur, 2 * a, 2 * b, m, e, 8)
+            vhi, vlo = capi.wavelet_apply(D, 8, 3, w, na=True)
+            k = b - a
+            np.testing.assert_allclose(bh[a:b].cpu().numpy(), vhi[:k], atol=1e-4)
+            np.testing.assert_allclose(bl[a:b].cpu().numpy(), vlo[:k], atol=1e-4)
+            np.testing.assert_allclose(out[off + a:off + b].cpu().numpy(), vhi[:k], atol=1e-4)
+            if lvl == 2:
+                np.testing.assert_allclose(out[off + half + a:off + half + b].cpu().numpy(),
+                                           vlo[:k], atol=1e-4)
+        cur, m, off = bl, half, off + half
+        del bh

@@ -3,7 +3,8 @@
 levels; effective bytes = input + output (the pyramid is len floats per
 signal), against a torch copy of the same volume in the same process.
 ORDERS=8 LEVELS=5 SIGNALS=65536 LEN=1024 ROUNDS=5 VEC=1,0 (vs_tune_set dwt_vec arms)
-THREADS=0 (dwt_threads arms, comma list; 0 = auto)"""
+THREADS=0 (dwt_threads arms, comma list; 0 = auto)
+SINGLE=1 times one decimated level (vs_dwt: hi and lo of len / 2) instead."""
 import ctypes
 import json
 import os
@@ -43,13 +44,21 @@ def main():
         timed(lambda: out.copy_(x)) for _ in range(rounds)) / 1e12, 2)}
     vecs = [int(a) for a in os.environ.get("VEC", "1,0").split(",")]
     thr = [int(a) for a in os.environ.get("THREADS", "0").split(",")]
+    for k in ("dwt_tile", "dwt_halo_div"):   # DWT_TILE / DWT_HALO_DIV: tiled-pass knobs
+        if os.environ.get(k.upper()):
+            assert lib.vs_tune_set(k.encode(), int(os.environ[k.upper()])) == 0
     for vec, nt, order in [(v, t, o) for v in vecs for t in thr for o in orders]:
         assert lib.vs_tune_set(b"dwt_vec", vec) == 0
         assert lib.vs_tune_set(b"dwt_threads", nt) == 0
 
         def run():
-            st = lib.vs_dwt_multilevel(0, order, levels, 0, ctypes.c_void_p(x.data_ptr()), n,
-                                       ctypes.c_void_p(out.data_ptr()), nsig, s)
+            if os.environ.get("SINGLE") == "1":
+                st = lib.vs_dwt(0, order, 0, ctypes.c_void_p(x.data_ptr()), n, n,
+                                ctypes.c_void_p(out.data_ptr()),
+                                ctypes.c_void_p(out.data_ptr() + 2 * n * nsig), n // 2, nsig, s)
+            else:
+                st = lib.vs_dwt_multilevel(0, order, levels, 0, ctypes.c_void_p(x.data_ptr()), n,
+                                           ctypes.c_void_p(out.data_ptr()), nsig, s)
             assert st == 0, lib.vs_last_error()
         t = statistics.median(timed(run) for _ in range(rounds))
         key = f"db{order}_vec{vec}" + (f"_t{nt}" if nt else "")
