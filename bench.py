@@ -8,7 +8,7 @@ aggregate GFLOP/s (weak scaling: every rank multiplies its own pair of
 matrices).  The second half of the metric, 1D convolution throughput at
 signal length 2^20 (filter 4096, batch 64 per GPU, auto-selected algorithm),
 is timed the same way and reported in `secondary`, as are two
-other BASELINE configurations: overlap-save convolution 2^22 x 4096 taps,
+other benchmark configurations of BASELINE.json: overlap-save convolution 2^22 x 4096 taps,
 batch 256 (config 3), row-split batched SGEMM 8192^2 x 64 (C row blocks
 all-gathered over RCCL / xGMI, config 5) and the SWT db8 x 8 levels over
 65536 signals sharded data-parallel (config 4).
@@ -39,7 +39,7 @@ CONV_BATCH = 64
 
 
 def _baseline():
-    """Reference numbers this run is divided by (None if none)."""
+    """Reference numbers this run is divided by (None if there are none)."""
     path = os.path.join(REPO, "bench", "reference_cpu_baseline.json")
     if os.path.exists(path):
         with open(path) as f:
@@ -205,7 +205,7 @@ def main():
             secondary["conv1d_plan_msamples_per_s"] = round(
                 CONV_LEN * CONV_BATCH * csteps * world / dtp / 1e6, 1)
         del x, y
-        # BASELINE config 3: overlap-save convolution, signal 2^22, filter
+        # benchmark config 3: overlap-save convolution, signal 2^22, filter
         # 4096, batch 256 (per GPU), per call and through a plan
         c3_len, c3_batch = 1 << 22, 256
         x3 = torch.randn((c3_batch, c3_len), device="cuda", generator=g)
@@ -246,7 +246,7 @@ def main():
                                   max(0, algo - 1)]},
         })
 
-    # ------------------------------------- comm-bearing BASELINE configs
+    # ------------------------------------- benchmark configs with communication
     # Config 5 (row-split batched SGEMM 8192^2 x 64, RCCL all-gather of the C
     # row blocks over xGMI, overlapped with the next matrix's GEMM: every rank
     # holds its rows of the 64 A matrices, all of B and the gathered C,
@@ -309,7 +309,7 @@ def main():
     base = _baseline()
     vs_base = None
     if base.get("sgemm_4096_gflops"):
-        # The reference publishes no numbers (BASELINE.md); this is its own
+        # The reference publishes no numbers; this is its own
         # AVX code measured on one host core (tools/measure_reference_cpu.py).
         vs_base = round(gflops / base["sgemm_4096_gflops"], 1)
         secondary["baseline_source"] = base.get("source")

@@ -1,5 +1,4 @@
-// The reference's own benchmark shapes (tests/benchmark.inc users, listed in
-// BASELINE.md rows 1-15) timed per call through the public C API.
+// The reference's own benchmark shapes (tests/benchmark.inc users) timed per call through the public C API.
 //
 // The same source is compiled twice (tools/bench_reference_shapes.py):
 //   * against the reference sources (src/*.c, -O2 -march=native; its

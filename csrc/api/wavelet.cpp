@@ -1,7 +1,7 @@
 // wavelet.h (reference src/wavelet.c).  wavelet_apply / stationary_wavelet_
 // apply run the HIP kernels of csrc/kernels/wavelet.hip; the *_na variants
 // are the host reference.  The "prepared array" helpers keep the reference's
-// non-AVX contract (the GPU needs no shifted copies, SURVEY.md §2.1 C20).
+// non-AVX contract (the GPU needs no shifted copies).
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include "simd/wavelet.h"
 

@@ -1,5 +1,4 @@
-// Multi-GPU layer of the C library (include/simd/dist.h; SURVEY.md §2.2 rows
-// D2-D5, §5 "Distributed comm backend").
+// Multi-GPU layer of the C library (include/simd/dist.h).
 //
 // One process drives all ranks.  Each rank = (device, main stream, side
 // stream).  Two backends implement the same collectives:
@@ -13,8 +12,7 @@
 //            form a communicator (shared devices, one GPU) and as the
 //            test double that exercises every sharding / halo path on a
 //            single GPU box (tests/test_dist.py).
-// The reference has no distributed code at all ("no
-// symbols"); these entry points are new, shaped after its single-device
+// The reference has no distributed code at all (no such symbols); these entry points are new, shaped after its single-device
 // APIs (src/convolve.c:381-395, src/wavelet.c:1907-1940, src/matrix.c:255).
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include "simd/dist.h"

@@ -1,4 +1,4 @@
-// Batched 1D convolution / cross-correlation (SURVEY.md §2.3 K9, K11, K12).
+// Batched 1D convolution / cross-correlation.
 //
 // Three algorithms, as in the reference (src/convolve.c), all on the GPU:
 //   * direct: LDS-tiled brute force.  A 256-thread block produces 2048
@@ -482,31 +482,15 @@ void launch_block_t(const BlockArgs &a, const float2 *tw, hipStream_t s) {
 }
 
 
-// Diagnostic build only (-DVS_CONV_STAMPS, tools/conv_stamps.py): per-phase
-// shader-clock stamps of wave 0 of every real-block workgroup, read back by
-// vs_conv_stamps().  Never compiled into the shipped library.
+// Diagnostic build only (make stamps, tools/conv_stamps.py): per-phase
+// shader-clock stamps of the real-block kernel; the hooks compile to nothing
+// in the shipped library and their code lives in csrc/diag/.
 #ifdef VS_CONV_STAMPS
-constexpr int kStampSlots = 8, kStampMax = 1 << 16;
-__device__ unsigned long long g_stamps[kStampMax * kStampSlots];
-#define VS_STAMP(i) stamp[i] = __builtin_amdgcn_s_memtime()
-// Residency probe: every 256-thread workgroup sleeps ~`spin` shader cycles;
-// VG forces the kernel to allocate >= VG VGPRs.  Elapsed time / (blocks per
-// CU x spin) tells how many workgroups the hardware keeps resident per CU.
-template <int VG>
-__global__ __launch_bounds__(256) void residency_kernel(float *out, long long spin) {
-  extern __shared__ float dyn[];
-  if constexpr (VG == 240) asm volatile("v_mov_b32 v239, 0" ::: "v239");
-  if constexpr (VG == 168) asm volatile("v_mov_b32 v167, 0" ::: "v167");
-  if constexpr (VG == 128) asm volatile("v_mov_b32 v127, 0" ::: "v127");
-  const long long t0 = __builtin_amdgcn_s_memtime();
-  while (__builtin_amdgcn_s_memtime() - t0 < spin) __builtin_amdgcn_s_sleep(8);
-  dyn[threadIdx.x] = threadIdx.x;
-  __syncthreads();
-  if (blockIdx.x == 0) out[threadIdx.x] = dyn[255 - threadIdx.x];
-}
-
+#include "csrc/diag/conv_stamps.inc"
 #else
+#define VS_STAMP_DECL()
 #define VS_STAMP(i)
+#define VS_STAMP_FLUSH()
 #endif
 
 // --------------------------------------- real-block fused convolution
@@ -673,9 +657,7 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())
   const float *xr = a.x + static_cast<long long>(sig) * a.xs;
   float *yr = a.y + static_cast<long long>(sig) * a.ys;
   const int st = blk * a.step - a.pre;
-#ifdef VS_CONV_STAMPS
-  unsigned long long stamp[kStampSlots] = {};
-#endif
+  VS_STAMP_DECL();
   VS_STAMP(0);
   float2 v[E];
   load_real<PL, BUF>(a, xr, st, t, v);
@@ -714,26 +696,7 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())
   fft::transform<PL, true, true>(v, lds, t, twi);
   VS_STAMP(4);
   store_real<PL, BUF>(a, yr, st, t, v);
-#ifdef VS_CONV_STAMPS
-  __builtin_amdgcn_s_waitcnt(0);
-  VS_STAMP(5);
-  if (threadIdx.x < 64) {
-    unsigned hw = 0, xcc = 0;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    stamp[6] = hw;
-    stamp[7] = xcc;
-    const long long wg = static_cast<long long>(blockIdx.y) * gridDim.x + blockIdx.x;
-    const int lane = threadIdx.x;
-    if (wg < kStampMax && lane < kStampSlots) {
-      unsigned long long val = 0;
-#pragma unroll
-      for (int i = 0; i < kStampSlots; i++)
-        if (lane == i) val = stamp[i];
-      g_stamps[wg * kStampSlots + lane] = val;
-    }
-  }
-#endif
+  VS_STAMP_FLUSH();
 }
 
 // P, Q of the real-block kernel, one launch per filter straight from the
@@ -1438,89 +1401,7 @@ using namespace vs;
 extern "C" {
 
 #ifdef VS_CONV_STAMPS
-__attribute__((visibility("default"))) vs_status vs_conv_stamps(unsigned long long *out,
-                                                                 int n) {
-  VS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(conv::g_stamps),
-                             sizeof(unsigned long long) * std::min(n, conv::kStampMax) *
-                                 conv::kStampSlots));
-  return VS_OK;
-}
-
-__global__ __launch_bounds__(256) void lds_census_kernel(float *out) {
-  extern __shared__ float dyn[];
-  dyn[threadIdx.x] = threadIdx.x;
-  __syncthreads();
-  out[threadIdx.x] = dyn[255 - threadIdx.x];
-}
-
-__attribute__((visibility("default"))) float vs_residency_probe(int lds, int vg, int blocks,
-                                                                long long spin) {
-  float *out = nullptr;
-  (void)hipMalloc(&out, 1024);
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0);
-  (void)hipEventCreate(&e1);
-  auto launch = [&] {
-    if (vg == 240)
-      hipLaunchKernelGGL(conv::residency_kernel<240>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
-    else if (vg == 168)
-      hipLaunchKernelGGL(conv::residency_kernel<168>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
-    else if (vg == 128)
-      hipLaunchKernelGGL(conv::residency_kernel<128>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
-    else
-      hipLaunchKernelGGL(conv::residency_kernel<0>, dim3(blocks), dim3(256), lds, nullptr, out, spin);
-  };
-  launch();
-  (void)hipDeviceSynchronize();
-  (void)hipEventRecord(e0, nullptr);
-  launch();
-  (void)hipEventRecord(e1, nullptr);
-  (void)hipEventSynchronize(e1);
-  float ms = -1;
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  (void)hipFree(out);
-  return ms;
-}
-
-// occupancy the runtime reports for a 256-thread kernel with `lds` bytes of
-// dynamic LDS (diagnostics)
-__attribute__((visibility("default"))) int vs_lds_occupancy(int lds) {
-  int n = -1;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &n, reinterpret_cast<const void *>(&lds_census_kernel), 256, lds);
-  return n;
-}
-
-// hipFuncGetAttributes of a real-block kernel: {numRegs, sharedSizeBytes,
-// localSizeBytes, maxThreadsPerBlock, binaryVersion} (diagnostics)
-__attribute__((visibility("default"))) int vs_conv_attrs(int which, int *out) {
-  hipFuncAttributes at{};
-  const void *f = which == 0
-                      ? reinterpret_cast<const void *>(&conv::real_conv_kernel<13, 32, true>)
-                      : reinterpret_cast<const void *>(&conv::residency_kernel<240>);
-  const hipError_t e = hipFuncGetAttributes(&at, f);
-  out[0] = at.numRegs;
-  out[1] = static_cast<int>(at.sharedSizeBytes);
-  out[2] = static_cast<int>(at.localSizeBytes);
-  out[3] = at.maxThreadsPerBlock;
-  out[4] = at.binaryVersion;
-  return e;
-}
-
-// occupancy the runtime reports for the real-block kernels (diagnostics)
-__attribute__((visibility("default"))) int vs_conv_occupancy(int which) {
-  int n = -1;
-  if (which == 0)
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void *>(&conv::real_conv_kernel<13, 32, true>), 256, 0);
-  else if (which == 1)
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void *>(&conv::real_conv_kernel<13, 16, true>), 512, 0);
-  else
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void *>(&conv::real_conv_kernel<12, 0, true>), 256, 0);
-  return n;
-}
+#include "csrc/diag/conv_probes.inc"
 #endif
 
 int vs_conv1d_select(int64_t xlen, int hlen, int batch) {

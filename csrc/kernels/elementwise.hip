@@ -1,6 +1,5 @@
 // Elementwise CDNA4 kernels: dtype conversions, real/complex arithmetic,
-// fills, reversed copies and transcendental math (SURVEY.md §2.3 K1-K4, K7,
-// K16).  These are HBM-bound; every kernel moves 4 elements per lane per
+// fills, reversed copies and transcendental math.  These are HBM-bound; every kernel moves 4 elements per lane per
 // iteration with one vector load/store per operand (16 B for fp32) when the
 // pointers allow it, one vector per lane (grid-stride only past 2^20 blocks), and
 // falls back to a scalar body for unaligned operands.

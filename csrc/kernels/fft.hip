@@ -1,4 +1,4 @@
-// Radix-16/8/4/2 Stockham FFT for CDNA4 (SURVEY.md §2.3 K10; replaces the
+// Radix-16/8/4/2 Stockham FFT for CDNA4 (replaces the
 // reference's external FFTF, reference src/convolve.c:131-143).
 //
 //   * n <= 16384: one workgroup per signal (several per workgroup for small

@@ -1,4 +1,4 @@
-// LDS-resident Stockham FFT building blocks for CDNA4 (SURVEY.md §2.3 K10).
+// LDS-resident Stockham FFT building blocks for CDNA4.
 //
 // One signal of N = 2^LOGN complex points (N <= 16384) lives in LDS
 // (float2, XOR-swizzled within 16-element rows -- see lds_slot -- so the

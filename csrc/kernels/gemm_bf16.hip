@@ -1,5 +1,4 @@
-// bf16 matrix-core GEMM and the "bf16x3" fast-fp32 mode (SURVEY.md §2.3 K8:
-// "optional bf16x3 / bf16 MFMA modes"; build plan §7.2 step 4).
+// bf16 matrix-core GEMM and the "bf16x3" fast-fp32 mode.
 //
 //   vs_gemm_bf16:   C(fp32) = alpha op(A) op(B) + beta C, A/B bf16.
 //   vs_sgemm_ex(VS_GEMM_BF16X3, ...): fp32 operands split as x = hi + lo
@@ -17,7 +16,7 @@
 // (gemm_glds_kernel) stages both images global -> LDS with
 // global_load_lds_dwordx4 into two XOR-swizzled stages and runs
 // v_mfma_f32_32x32x16_bf16 on 256 x 256 (bf16) / 256 x 128 (bf16x3) tiles,
-// or 128 x 128 tiles when the large ones cannot fill every CU.  (Round-1
+// or 128 x 128 tiles when the large ones cannot fill every CU.  (Earlier
 // register-staged, three/four-stage ring and transposed-read variants were
 // measured slower or spilled and are in git history,
 // profiles/r1/gemm_modes_v*.log.)

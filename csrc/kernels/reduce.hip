@@ -1,4 +1,4 @@
-// Reductions and uint8 normalisation (SURVEY.md §2.3 K5, K6).
+// Reductions and uint8 normalisation.
 //
 // Deterministic two-pass reductions: pass 1 is a grid of at most 1024
 // blocks, each reducing its grid-stride share with 16-byte loads, a

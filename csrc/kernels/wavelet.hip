@@ -1,5 +1,5 @@
-// Decimated and stationary (a trous) wavelet transforms (SURVEY.md §2.3 K13,
-// K14) over the Daubechies / Symlet / Coiflet banks.
+// Decimated and stationary (a trous) wavelet transforms
+// over the Daubechies / Symlet / Coiflet banks.
 //
 //   * single level (vs_dwt / vs_swt): a 256-thread block owns a tile of 1024
 //     outputs of one signal, stages the input window (tile + filter support,
@@ -203,101 +203,12 @@ __global__ __launch_bounds__(256) void swt_multi_kernel(
   for (int i = threadIdx.x; i < len; i += blockDim.x) lrow[i] = in[i];
 }
 
-// Same transform, compile-time filter length and four consecutive outputs per
-// lane (len % 4 == 0): taps unrolled into registers, 16-byte LDS reads of the
-// input window (one window for dilation 1 and 2, one float4 per tap from
-// dilation 4 on) and 16-byte stores of hi and of the next level's input --
-// the store stream (levels + 1 rows per signal) is what bounds this kernel.
-template <int ORDER>
-__global__ __launch_bounds__(256) void swt_multi4_kernel(
-    Taps taps, int ext, int levels, const float *__restrict__ src, int len,
-    float *__restrict__ hi, float *__restrict__ lo) {
-  extern __shared__ __attribute__((aligned(16))) float smem4[];
-  // + 2 ORDER + 8: the dilation-1/2 window reads up to 2 (ORDER - 1) + 7
-  // floats past the last output (values beyond the halo are never used)
-  const int stride = (len + ((ORDER - 1) << (levels - 1)) + 2 * ORDER + 8 + 3) & ~3;
-  float *band0 = smem4, *band1 = smem4 + stride;
-  const int64_t sig = blockIdx.x;
-  float hp[ORDER], lp[ORDER];
-#pragma unroll
-  for (int r = 0; r < ORDER; r++) {
-    hp[r] = taps.hp[r];
-    lp[r] = taps.lp[r];
-  }
-  const float4 *x4 = reinterpret_cast<const float4 *>(src + sig * len);
-  for (int i = threadIdx.x; i < len / 4; i += blockDim.x)
-    reinterpret_cast<float4 *>(band0)[i] = x4[i];
-  float *in = band0, *out = band1;
-  for (int l = 0; l < levels; l++) {
-    const int dil = 1 << l;
-    const int halo = (ORDER - 1) * dil;
-    __syncthreads();
-    for (int t = threadIdx.x; t < halo; t += blockDim.x) {
-      const int j = ext_index(len + t, len, ext);
-      in[len + t] = j < 0 ? 0.f : in[j];
-    }
-    __syncthreads();
-    float4 *hrow = reinterpret_cast<float4 *>(hi + (sig * levels + l) * len);
-    for (int q = threadIdx.x; q < len / 4; q += blockDim.x) {
-      const int i0 = 4 * q;
-      float sh[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
-      if (dil <= 2) {
-        // window in[i0 .. i0 + 3 + 2 (ORDER - 1)], read as float4s
-        constexpr int W = (4 + 2 * (ORDER - 1) + 3) / 4;
-        float w[4 * W];
-#pragma unroll
-        for (int c = 0; c < W; c++) {
-          const float4 v = reinterpret_cast<const float4 *>(in + i0)[c];
-          w[4 * c] = v.x;
-          w[4 * c + 1] = v.y;
-          w[4 * c + 2] = v.z;
-          w[4 * c + 3] = v.w;
-        }
-        if (dil == 1) {
-#pragma unroll
-          for (int r = 0; r < ORDER; r++)
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-              sh[e] = fmaf(hp[r], w[r + e], sh[e]);
-              sl[e] = fmaf(lp[r], w[r + e], sl[e]);
-            }
-        } else {
-#pragma unroll
-          for (int r = 0; r < ORDER; r++)
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-              sh[e] = fmaf(hp[r], w[2 * r + e], sh[e]);
-              sl[e] = fmaf(lp[r], w[2 * r + e], sl[e]);
-            }
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < ORDER; r++) {
-          const float4 v = *reinterpret_cast<const float4 *>(in + i0 + r * dil);
-          const float ve[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int e = 0; e < 4; e++) {
-            sh[e] = fmaf(hp[r], ve[e], sh[e]);
-            sl[e] = fmaf(lp[r], ve[e], sl[e]);
-          }
-        }
-      }
-      hrow[q] = make_float4(sh[0], sh[1], sh[2], sh[3]);
-      reinterpret_cast<float4 *>(out)[q] = make_float4(sl[0], sl[1], sl[2], sl[3]);
-    }
-    float *t = in;
-    in = out;
-    out = t;
-  }
-  __syncthreads();
-  float4 *lrow = reinterpret_cast<float4 *>(lo + sig * len);
-  for (int q = threadIdx.x; q < len / 4; q += blockDim.x)
-    lrow[q] = reinterpret_cast<const float4 *>(in)[q];
-}
-
-// Round-2 multi-level kernel.  Same mapping as
-// swt_multi4_kernel, but the boundary extension of the next level's input is
-// written by the lanes that produce it, in the same pass:
+// All levels of one signal in LDS with compile-time filter length and four
+// consecutive outputs per lane (len % 4 == 0): taps in registers, 16-byte LDS
+// reads of the input window (one window for dilation 1 and 2, one float4 per
+// tap from dilation 4 on), 16-byte stores.  The boundary extension of the
+// next level's input is written by the lanes that produce it, in the same
+// pass:
 //   periodic: in[len + t] = in[t]          -> the float4 at i0 < halo is also
 //                                              stored at len + i0;
 //   mirror:   in[len + t] = in[len - 1 - t] -> the float4 at i0 is stored
@@ -307,9 +218,9 @@ __global__ __launch_bounds__(256) void swt_multi4_kernel(
 // No modulo / per-element extension code runs, each level costs one barrier,
 // and the last level writes the low band straight to HBM.  Needs
 // len % 4 == 0.
-// PMC (db16, 16384 x 1024): the old kernel issued ~4x the VALU instructions
-// of its FMAs, most of them in the modulo halo fill
-// (profiles/r2/swt/README.md).
+// PMC (db16, 16384 x 1024): a kernel with a separate modulo halo fill per
+// level issued ~4x the VALU instructions of its FMAs, most of them in that
+// fill (profiles/r2/swt/README.md).
 template <int ORDER, bool NT>
 __global__ __launch_bounds__(256) void swt_fused_kernel(
     Taps taps, int ext, int levels, const float *__restrict__ src, int len,
@@ -561,13 +472,14 @@ vs_status launch_swt_tiled(const Taps &t, int ext, int levels, const float *src,
   return VS_OK;
 }
 
-// Tuning knobs (vs_tune_set): "swt_fused" 0 = round-1 multi4 kernel,
-// 1 (default) = fused-extension kernel; "swt_nt" 1 (default) = non-temporal
+// Tuning knobs (vs_tune_set): "swt_fused" 0 = the scalar kernels
+// (swt_multi_kernel, level by level for long rows), 1 (default) = the
+// fused-extension and tiled kernels; "swt_nt" 1 (default) = non-temporal
 // hi stores (+3 % on db8 x 8 levels: the hi rows are never re-read here).
 thread_local int g_swt_fused = 1;
 thread_local int g_swt_nt = 1;
 // "dwt_vec" 1 (default) = vectorised pyramid kernel (dwt_multi4_kernel),
-// 0 = the scalar round-1 kernel.
+// 0 = the scalar kernel.
 thread_local int g_dwt_vec = 1;
 // "dwt_threads": workgroup size of the vectorised pyramid (0 = auto).
 thread_local int g_dwt_threads = 0;
@@ -580,22 +492,6 @@ thread_local int g_dwt_threads = 0;
 constexpr int kDwtTile = 4096;
 constexpr int kDwtHaloDiv = 16;
 thread_local int g_dwt_tile = kDwtTile, g_dwt_halo_div = kDwtHaloDiv;
-
-template <int ORDER>
-vs_status launch_swt_multi4(const Taps &t, int ext, int levels, const float *src, int len,
-                            float *hi, float *lo, int batch, hipStream_t s) {
-  const int halo = (ORDER - 1) << (levels - 1);
-  const size_t lds =
-      2 * static_cast<size_t>((len + halo + 2 * ORDER + 8 + 3) & ~3) * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(swt_multi4_kernel<ORDER>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (kMultiMax + kMultiExt + 2 * 30 + 12) * 4);
-  VS_HIP(attr);
-  hipLaunchKernelGGL(swt_multi4_kernel<ORDER>, dim3(static_cast<unsigned>(batch)), dim3(256),
-                     lds, s, t, ext, levels, src, len, hi, lo);
-  VS_HIP(hipGetLastError());
-  return VS_OK;
-}
 
 // Mallat pyramid of one signal in LDS: out row = [hi_1 | hi_2 | ... | hi_L | lo_L].
 constexpr int kDwtMultiMax = 16384;
@@ -686,7 +582,7 @@ __global__ __launch_bounds__(256) void dwt_multi_t_kernel(
   for (int k = threadIdx.x; k < n; k += blockDim.x) orow[off + k] = in[k];
 }
 
-// Vectorised pyramid (round 2): float4 input loads, four consecutive outputs
+// Vectorised pyramid: float4 input loads, four consecutive outputs
 // per lane from a float4 register window (inputs 2k .. 2k + 6 + ORDER - 1),
 // float4 hi stores and low-band writes; the two LDS bands are len and len / 2
 // (+ pads) so three 8192-sample workgroups share a CU.  Levels whose half
@@ -1141,16 +1037,6 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
       VS_SWTF(2) VS_SWTF(4) VS_SWTF(6) VS_SWTF(8) VS_SWTF(10) VS_SWTF(12) VS_SWTF(14)
       VS_SWTF(16) VS_SWTF(18) VS_SWTF(20) VS_SWTF(24) VS_SWTF(30)
 #undef VS_SWTF
-      default: break;
-    }
-  }
-  if (len <= kMultiMax && halo <= kMultiExt && len % 4 == 0) {
-    switch (order) {
-#define VS_SWT4(O) \
-  case O: return launch_swt_multi4<O>(t, ext, levels, src, len, hi, lo, batch, s);
-      VS_SWT4(2) VS_SWT4(4) VS_SWT4(6) VS_SWT4(8) VS_SWT4(10) VS_SWT4(12) VS_SWT4(14)
-      VS_SWT4(16) VS_SWT4(18) VS_SWT4(20) VS_SWT4(24) VS_SWT4(30)
-#undef VS_SWT4
       default: break;
     }
   }

@@ -360,7 +360,7 @@ namespace {
 //   * re-read inputs (convolution windows, GEMM panels, read by many
 //     workgroups): packed into the pinned image and sent to the device
 //     image with ONE host->device copy before the first kernel reads them.
-// Round 1 staged every operand through its own pageable copy (HIP bounces
+// Staging every operand through its own pageable copy (HIP bounces
 // each through an internal buffer) and ended with a blocking stream
 // synchronise: ~40-65 us per call.
 struct Arena {

@@ -1,8 +1,7 @@
 // Runtime services shared by every API layer: device discovery, error
 // reporting, stream-ordered scratch memory, host<->device staging, logging.
 //
-// The reference has no runtime (everything is a synchronous host call,
-// SURVEY.md §3); this layer is what lets the source-compatible host API drive
+// The reference has no runtime (everything is a synchronous host call); this layer is what lets the source-compatible host API drive
 // MI355X kernels: it decides where a call runs, stages host operands through
 // the library's own non-blocking stream and synchronises before returning.
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.

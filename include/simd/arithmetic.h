@@ -16,8 +16,8 @@
  *  The *_na functions are the scalar reference semantics (reference
  *  arithmetic.h:43-191) and always run on the host.
  *
- *  Semantics follow the scalar reference, not its SIMD quirks (SURVEY.md
- *  App. A): int16 inputs are sign-extended in order; float -> int conversion
+ *  Semantics follow the scalar reference, not its SIMD quirks:
+ *  int16 inputs are sign-extended in order; float -> int conversion
  *  truncates toward zero; narrowing to int16 saturates (the tests only use
  *  in-range values, where this equals the reference cast).
  *  Copyright 2026 veles.simd_amd authors. Apache-2.0.

@@ -6,7 +6,7 @@
  *  2012) defines register-level AVX functions: log256_ps (:161),
  *  exp256_ps (:247), sin256_ps (:327), cos256_ps (:454), sincos256_ps
  *  (:571) and pow256_ps (:720) on __m256.  There is no host SIMD path in
- *  this library (SURVEY.md §0): a 64-lane wavefront replaces the 8-lane
+ *  this library: a 64-lane wavefront replaces the 8-lane
  *  register, so the same functions are offered over arrays, evaluated on the
  *  GPU for simd != 0 (OCML sincosf; pow evaluated in double and rounded once,
  *  <= 1 ulp against double)

@@ -2,8 +2,8 @@
  *  @brief Multi-GPU layer of the C library: one process drives every local
  *  MI355X ("single-process, multi-device"), RCCL over xGMI for collectives.
  *
- *  The reference has no parallelism beyond SIMD lanes; this
- *  header is the native counterpart of its rows D2-D5:
+ *  The reference has no parallelism beyond SIMD lanes; this header adds the
+ *  parallel forms of its operations:
  *    - D2 data parallel:     vs_dist_conv1d_batch (batch sharded over ranks);
  *    - D3 tensor parallel:   vs_dist_sgemm_rowsplit (A rows sharded, B
  *                            broadcast, C rows downloaded per rank) and
@@ -93,7 +93,7 @@ vs_status vs_dist_sgemm_rowsplit(vs_dist_t ctx, int m, int n, int k,
                                  const float *A, const float *B, float *C,
                                  int batch);
 /// Device-resident form for consumers that need the whole product on every
-/// GPU (BASELINE config 5): A[r] is rank r's rows ([batch][rows_r][k] on
+/// GPU (benchmark config 5): A[r] is rank r's rows ([batch][rows_r][k] on
 /// its device, rows_r from vs_dist_shard(m, size, r)), B[r] the full
 /// [batch][k][n] on rank r, C[r] a [batch][m][n] buffer on rank r.  Each
 /// rank computes its rows in place in its C[r]; the row blocks of matrix b

@@ -1,6 +1,6 @@
 /*! @file gpu.h
  *  @brief Device-pointer, batched and stream-ordered API (no reference
- *  counterpart; SURVEY.md App. B "New").
+ *  counterpart).
  *
  *  Every vs_* compute function takes device pointers and a stream (a
  *  hipStream_t passed as void*; NULL is the HIP null stream) and is

@@ -92,8 +92,7 @@ def test_per_signal_filters_real_block():
 @pytest.mark.parametrize("corr", [False, True])
 def test_partitioned_long_filters(xlen, hlen, batch, corr):
     """Filters of 9000-12345 taps, explicit OS request: one L = 32768 real
-    block since round 2 (partitions before; test_partitioned_beyond_32768_block
-    keeps the partitioned path covered)."""
+    block (test_partitioned_beyond_32768_block covers the partitioned path)."""
     _check(xlen, hlen, batch, "overlap_save", corr)
 
 
@@ -106,7 +105,7 @@ def test_per_signal_filters_beyond_one_block():
 @pytest.mark.slow
 @pytest.mark.parametrize("xlen,hlen", [(1 << 25, 20000), (1 << 23, 65536)])
 def test_cliff_shapes(xlen, hlen):
-    """VERDICT r1 item 3 shapes: both exceeded the 2^24 FFT before."""
+    """Shapes past the largest single transform (2^24 points)."""
     from veles.simd_amd import _lib
     assert _lib.lib().vs_conv1d_select(xlen, hlen, 1) in (2, 3)
     _check(xlen, hlen, 1, "auto", False)

@@ -1,8 +1,8 @@
-"""Native multi-GPU layer (csrc/dist/dist.cpp) -- SURVEY.md §2.2 rows D2-D5.
+"""Native multi-GPU layer (csrc/dist/dist.cpp).
 
 CPU: the shard arithmetic and the no-GPU error path.  GPU: every collective
 and sharded entry point with the LOCAL backend at 1-4 virtual ranks sharing
-one MI355X (the in-process fake communicator of SURVEY.md §4 item 4), plus the
+one MI355X (an in-process fake communicator), plus the
 RCCL backend over the devices present (one rank per device).  Oracles: numpy
 float64 and the single-device host reference (`*_na`) of the same op.
 """
@@ -202,7 +202,7 @@ def test_swt_long(world, ext):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", WORLDS)
 def test_swt_dwt_batch(world):
-    """Data-parallel wavelet batches (BASELINE config 4's sharding): uneven
+    """Data-parallel wavelet batches (the sharding of the SWT benchmark config): uneven
     shards (batch 11), against the single-device op."""
     import torch
     from veles.simd_amd import ops

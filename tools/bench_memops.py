@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Bandwidth of the memory-bound kernels at
+"""Bandwidth of the memory-bound kernels (elementwise, reductions, normalisation, peaks) at
 2^26 elements against same-process HBM ceilings (torch fill_ = write-only,
 copy_ = read + write).  Bytes are the minimum each op must move (inputs read
 once, outputs written once).  Every op is timed after bench.py's clock-ramp

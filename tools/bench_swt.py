@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""SWT multi-level throughput (BASELINE config 4 shape: db8, 8 levels,
+"""SWT multi-level throughput (benchmark config 4 shape: db8, 8 levels,
 signals x 1024) against the HBM ceilings measured in the same process:
 a write-only fill and a read+write copy of the same byte volume (torch).
 Effective bytes = input + levels hi rows + final lo (each fp32).

@@ -18,7 +18,7 @@ The reference ships its banks as literal tables (``src/daubechies.c:34``,
   moments about tap 2N), started from 6-digit seeds of the classical
   coefficients (Daubechies, *Ten Lectures*, Table 8.1) and refined to 40 digits.
 
-Normalisation follows the reference contract (``SURVEY.md`` App. A):
+Normalisation follows the reference contract (reference src/wavelet.c filter tables):
 Daubechies rows sum to sqrt(2); Symlet and Coiflet rows sum to 1.
 
 Output: ``csrc/data/wavelet_tables.cpp`` (flat per-family arrays, row ``k``

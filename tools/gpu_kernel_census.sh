@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Kernel census of the GPU test suite (VERDICT r1 item 4): first the
+# Kernel census of the GPU test suite: first the
 # reference-shape device tests alone, then `pytest -m gpu` under
 # rocprofv3 --kernel-trace --stats; tools/kernel_census.py turns the stats
 # into profiles/r2/gpu_suite_kernels.md.

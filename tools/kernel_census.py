@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace --stats run of `pytest -m gpu` into a
 markdown census of the library's kernels (which of our kernels the GPU suite
-launched, how often, total time), grouped by the SURVEY kernel rows K1-K16.
+launched, how often, total time), grouped by kernel family (rows K1-K16 of docs/ARCHITECTURE.md).
 
 Usage: tools/kernel_census.py <dir with *_kernel_stats.csv> > out.md"""
 import csv
@@ -10,7 +10,7 @@ import os
 import re
 import sys
 
-# SURVEY.md §2.3 kernel rows -> name patterns of our kernels
+# kernel family rows -> name patterns of our kernels
 ROWS = [
     ("K1 conversions", r"Convert<"),
     ("K2 fp16->fp32", r"Convert<unsigned short, float>"),
@@ -60,7 +60,7 @@ def main():
     print("# Kernels launched by `pytest -m gpu` (rocprofv3 --kernel-trace --stats)\n")
     print(f"{len(ours)} distinct kernels of this library, {sum(r[1] for r in ours)} launches; "
           f"{len(rows) - len(ours)} other kernels (PyTorch / runtime).\n")
-    print("| SURVEY row | kernels hit | launches |\n|---|---|---|")
+    print("| kernel row | kernels hit | launches |\n|---|---|---|")
     for label, pat in ROWS:
         hit = [r for r in ours if re.search(pat, r[0])]
         print(f"| {label} | {len(hit)} | {sum(r[1] for r in hit)} |")

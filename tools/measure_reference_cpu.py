@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Measure the reference library's own CPU code on the BASELINE shapes.
 
-The reference publishes no numbers (BASELINE.md).  This compiles the
+The reference publishes no numbers.  This compiles the
 reference sources (read-only mount /root/reference) with its documented
 flags (-O2 -march=native, common.ac:267) into a scratch directory and times
   * matrix_multiply(simd=1, ...) at 4096^3 (its AVX GEMM, one core),

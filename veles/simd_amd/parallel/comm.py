@@ -4,8 +4,8 @@ Every multi-GPU feature of veles.simd_amd runs as N processes (one per GPU,
 launched by ``torch.distributed.run``) talking over RCCL -- the "nccl"
 backend of PyTorch-ROCm -- which routes collectives over the xGMI links of an
 MI355X node.  CPU tensors use "gloo" so the same code paths are testable
-without GPUs.  The reference library has no distributed layer at all
-(SURVEY.md §2.2); this module is new.
+without GPUs.  The reference library has no distributed layer at all;
+this module is new.
 """
 from __future__ import annotations
 

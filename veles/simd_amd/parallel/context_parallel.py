@@ -1,5 +1,4 @@
-"""Sequence ("context") parallelism for very long 1-D signals (SURVEY.md §5,
-D4).
+"""Sequence ("context") parallelism for very long 1-D signals .
 
 A signal too long for one GPU (or just long enough that 8 GPUs finish it 8x
 faster) is split into contiguous chunks, one per rank.  The only coupling is

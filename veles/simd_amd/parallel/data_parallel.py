@@ -1,4 +1,4 @@
-"""Data parallelism over the batch dimension (SURVEY.md §2.2, D2).
+"""Data parallelism over the batch dimension.
 
 Batched primitives (conv1d over many signals, SWT over 65536 signals, batched
 SGEMM) are embarrassingly parallel over the batch: each rank processes its

@@ -4,7 +4,7 @@ include/simd/dist.h): one process drives every local MI355X, RCCL over xGMI
 also lets several ranks share one GPU -- the single-GPU test double).
 
 This is the counterpart of the torch.distributed helpers in this package for
-C-API users (one process, many devices) -- SURVEY.md §2.2 row D5.
+C-API users (one process, many devices).
 """
 from __future__ import annotations
 

@@ -1,4 +1,4 @@
-"""1-D row-split batched SGEMM over ranks (BASELINE
+"""1-D row-split batched SGEMM over ranks (benchmark
 config 5: batched SGEMM 8192^2 x 64 row-split across 8 GPUs with an RCCL
 all-gather over xGMI).
 

@@ -1,8 +1,7 @@
 """Runtime configuration knobs: the environment variables read by the native
 library (csrc/) and the Python layer, with their defaults and meaning.
 
-The reference is configured only at build time (autotools flags, SURVEY.md
-§5); these are the runtime equivalents.  ``KNOBS`` is the single registry:
+The reference is configured only at build time (autotools flags); these are the runtime equivalents.  ``KNOBS`` is the single registry:
 tests/test_config.py checks that every variable the native sources read is
 listed here, and ``python -m veles.simd_amd.utils.config`` prints the
 effective values of the current environment."""
