@@ -221,14 +221,19 @@ __global__ __launch_bounds__(256) void swt_multi_kernel(
 // PMC (db16, 16384 x 1024): a kernel with a separate modulo halo fill per
 // level issued ~4x the VALU instructions of its FMAs, most of them in that
 // fill (profiles/r2/swt/README.md).
-template <int ORDER, bool NT>
+template <int ORDER, bool NT, int SIGS>
 __global__ __launch_bounds__(256) void swt_fused_kernel(
     Taps taps, int ext, int levels, const float *__restrict__ src, int len,
-    float *__restrict__ hi, float *__restrict__ lo) {
+    float *__restrict__ hi, float *__restrict__ lo, int batch) {
+  // SIGS signals per workgroup, interleaved lane by lane: every lane carries
+  // SIGS independent float4 chains through each level and the level barrier
+  // is shared.
   extern __shared__ __attribute__((aligned(16))) float smemf[];
   const int stride = (len + ((ORDER - 1) << (levels - 1)) + 2 * ORDER + 8 + 3) & ~3;
-  float *band0 = smemf, *band1 = smemf + stride;
-  const int64_t sig = blockIdx.x;
+  // a last workgroup short of signals repeats the last one (same values
+  // written twice) so the SIGS chains stay branch-free
+  const int64_t sig0 = static_cast<int64_t>(blockIdx.x) * SIGS;
+  const int64_t sig_last = batch - 1;
   const int len4 = len >> 2;
   float hp[ORDER], lp[ORDER];
 #pragma unroll
@@ -238,9 +243,9 @@ __global__ __launch_bounds__(256) void swt_fused_kernel(
   }
   if (ext == EXTENSION_TYPE_ZERO) {
     const int z4 = (stride - len) >> 2;
-    for (int i = threadIdx.x; i < 2 * z4; i += blockDim.x)
-      reinterpret_cast<float4 *>(i < z4 ? band0 + len : band1 + len)[i < z4 ? i : i - z4] =
-          make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int b = 0; b < 2 * SIGS; b++)
+      for (int i = threadIdx.x; i < z4; i += blockDim.x)
+        reinterpret_cast<float4 *>(smemf + b * stride + len)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // Stores the float4 `v` at output position i0 of band `b` plus its image in
   // the extension region for a consumer needing `halo` extension samples.
@@ -257,108 +262,135 @@ __global__ __launch_bounds__(256) void swt_fused_kernel(
         reinterpret_cast<float4 *>(b + len + t)[0] = r;
     }
   };
-  const float4 *x4 = reinterpret_cast<const float4 *>(src + sig * len);
-  for (int q = threadIdx.x; q < len4; q += blockDim.x) put(band0, 4 * q, x4[q], ORDER - 1);
-  float *in = band0, *out = band1;
+  // bands of signal g: smemf + (2 g + parity) stride
+#pragma unroll
+  for (int g = 0; g < SIGS; g++) {
+    const float4 *x4 =
+        reinterpret_cast<const float4 *>(src + min(sig0 + g, sig_last) * len);
+    for (int q = threadIdx.x; q < len4; q += blockDim.x)
+      put(smemf + 2 * g * stride, 4 * q, x4[q], ORDER - 1);
+  }
+  int par = 0;
   for (int l = 0; l < levels; l++) {
     const int dil = 1 << l;
-    lds_barrier();  // input band and its extension complete
+    lds_barrier();  // input bands and their extensions complete
     if (ext == EXTENSION_TYPE_CONSTANT) {
-      const float c = in[len - 1];
-      for (int t = threadIdx.x; t < (ORDER - 1) * dil; t += blockDim.x) in[len + t] = c;
+      for (int g = 0; g < SIGS; g++) {
+        float *in = smemf + (2 * g + par) * stride;
+        const float c = in[len - 1];
+        for (int t = threadIdx.x; t < (ORDER - 1) * dil; t += blockDim.x) in[len + t] = c;
+      }
       lds_barrier();
     }
     const bool last = l == levels - 1;
     const int next_halo = (ORDER - 1) * dil * 2;
-    float4 *hrow = reinterpret_cast<float4 *>(hi + (sig * levels + l) * len);
     for (int q = threadIdx.x; q < len4; q += blockDim.x) {
       const int i0 = 4 * q;
-      float sh[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
-      if (dil <= 2) {
-        constexpr int W = (4 + 2 * (ORDER - 1) + 3) / 4;
-        float w[4 * W];
 #pragma unroll
-        for (int c = 0; c < W; c++) {
-          const float4 v = reinterpret_cast<const float4 *>(in + i0)[c];
-          w[4 * c] = v.x;
-          w[4 * c + 1] = v.y;
-          w[4 * c + 2] = v.z;
-          w[4 * c + 3] = v.w;
-        }
-        if (dil == 1) {
+      for (int g = 0; g < SIGS; g++) {
+        const float *in = smemf + (2 * g + par) * stride;
+        float *out = smemf + (2 * g + (par ^ 1)) * stride;
+        const int64_t sig = min(sig0 + g, sig_last);
+        float sh[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
+        if (dil <= 2) {
+          constexpr int W = (4 + 2 * (ORDER - 1) + 3) / 4;
+          float w[4 * W];
 #pragma unroll
-          for (int r = 0; r < ORDER; r++)
+          for (int c = 0; c < W; c++) {
+            const float4 v = reinterpret_cast<const float4 *>(in + i0)[c];
+            w[4 * c] = v.x;
+            w[4 * c + 1] = v.y;
+            w[4 * c + 2] = v.z;
+            w[4 * c + 3] = v.w;
+          }
+          if (dil == 1) {
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-              sh[e] = fmaf(hp[r], w[r + e], sh[e]);
-              sl[e] = fmaf(lp[r], w[r + e], sl[e]);
-            }
+            for (int r = 0; r < ORDER; r++)
+#pragma unroll
+              for (int e = 0; e < 4; e++) {
+                sh[e] = fmaf(hp[r], w[r + e], sh[e]);
+                sl[e] = fmaf(lp[r], w[r + e], sl[e]);
+              }
+          } else {
+#pragma unroll
+            for (int r = 0; r < ORDER; r++)
+#pragma unroll
+              for (int e = 0; e < 4; e++) {
+                sh[e] = fmaf(hp[r], w[2 * r + e], sh[e]);
+                sl[e] = fmaf(lp[r], w[2 * r + e], sl[e]);
+              }
+          }
         } else {
 #pragma unroll
-          for (int r = 0; r < ORDER; r++)
+          for (int r = 0; r < ORDER; r++) {
+            const float4 v = *reinterpret_cast<const float4 *>(in + i0 + r * dil);
+            const float ve[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-              sh[e] = fmaf(hp[r], w[2 * r + e], sh[e]);
-              sl[e] = fmaf(lp[r], w[2 * r + e], sl[e]);
+              sh[e] = fmaf(hp[r], ve[e], sh[e]);
+              sl[e] = fmaf(lp[r], ve[e], sl[e]);
             }
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < ORDER; r++) {
-          const float4 v = *reinterpret_cast<const float4 *>(in + i0 + r * dil);
-          const float ve[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int e = 0; e < 4; e++) {
-            sh[e] = fmaf(hp[r], ve[e], sh[e]);
-            sl[e] = fmaf(lp[r], ve[e], sl[e]);
           }
         }
+        const float4 hv = make_float4(sh[0], sh[1], sh[2], sh[3]);
+        const float4 lv = make_float4(sl[0], sl[1], sl[2], sl[3]);
+        float4 *hrow = reinterpret_cast<float4 *>(hi + (sig * levels + l) * len);
+        if (NT) {
+          typedef float native4 __attribute__((ext_vector_type(4)));
+          const native4 nv = {hv.x, hv.y, hv.z, hv.w};
+          __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(hrow + q));
+        } else {
+          hrow[q] = hv;
+        }
+        if (last)
+          reinterpret_cast<float4 *>(lo + sig * len)[q] = lv;
+        else
+          put(out, i0, lv, next_halo);
       }
-      const float4 hv = make_float4(sh[0], sh[1], sh[2], sh[3]);
-      const float4 lv = make_float4(sl[0], sl[1], sl[2], sl[3]);
-      if (NT) {
-        typedef float native4 __attribute__((ext_vector_type(4)));
-        const native4 nv = {hv.x, hv.y, hv.z, hv.w};
-        __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(hrow + q));
-      }
-      else
-        hrow[q] = hv;
-      if (last)
-        reinterpret_cast<float4 *>(lo + sig * len)[q] = lv;
-      else
-        put(out, i0, lv, next_halo);
     }
-    float *t = in;
-    in = out;
-    out = t;
+    par ^= 1;
   }
+}
+
+// Signals per workgroup of the fused kernel (vs_tune_set("swt_sigs", 1 / 2)).
+extern thread_local int g_swt_sigs;
+
+template <int ORDER, bool NT, int SIGS>
+vs_status launch_swt_fused_t(const Taps &t, int ext, int levels, const float *src, int len,
+                             float *hi, float *lo, int batch, hipStream_t s) {
+  const int halo = (ORDER - 1) << (levels - 1);
+  const size_t lds =
+      2 * SIGS * static_cast<size_t>((len + halo + 2 * ORDER + 8 + 3) & ~3) * sizeof(float);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(swt_fused_kernel<ORDER, NT, SIGS>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  VS_HIP(attr);
+  hipLaunchKernelGGL((swt_fused_kernel<ORDER, NT, SIGS>),
+                     dim3(static_cast<unsigned>((batch + SIGS - 1) / SIGS)), dim3(256), lds, s, t,
+                     ext, levels, src, len, hi, lo, batch);
+  VS_HIP(hipGetLastError());
+  return VS_OK;
 }
 
 template <int ORDER>
 vs_status launch_swt_fused(const Taps &t, int ext, int levels, const float *src, int len,
                            float *hi, float *lo, int batch, bool nt, hipStream_t s) {
   const int halo = (ORDER - 1) << (levels - 1);
-  const size_t lds =
-      2 * static_cast<size_t>((len + halo + 2 * ORDER + 8 + 3) & ~3) * sizeof(float);
-  const void *fn = nt ? reinterpret_cast<const void *>(swt_fused_kernel<ORDER, true>)
-                      : reinterpret_cast<const void *>(swt_fused_kernel<ORDER, false>);
-  static const hipError_t attr0 = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(swt_fused_kernel<ORDER, false>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (kMultiMax + kMultiExt + 2 * 30 + 12) * 4);
-  static const hipError_t attr1 = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(swt_fused_kernel<ORDER, true>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (kMultiMax + kMultiExt + 2 * 30 + 12) * 4);
-  VS_HIP(attr0);
-  VS_HIP(attr1);
-  (void)fn;
-  if (nt)
-    hipLaunchKernelGGL((swt_fused_kernel<ORDER, true>), dim3(static_cast<unsigned>(batch)),
-                       dim3(256), lds, s, t, ext, levels, src, len, hi, lo);
-  else
-    hipLaunchKernelGGL((swt_fused_kernel<ORDER, false>), dim3(static_cast<unsigned>(batch)),
-                       dim3(256), lds, s, t, ext, levels, src, len, hi, lo);
-  VS_HIP(hipGetLastError());
-  return VS_OK;
+  const size_t one = 2 * static_cast<size_t>((len + halo + 2 * ORDER + 8 + 3) & ~3) * sizeof(float);
+  // several signals per workgroup while their bands fit the CU's LDS
+  int sigs = std::max(1, std::min(g_swt_sigs, batch));
+  while (sigs > 1 && sigs * one > 150 * 1024) sigs--;
+#define VS_SWT_SIGS(N)                                                                          \
+  case N:                                                                                       \
+    return nt ? launch_swt_fused_t<ORDER, true, N>(t, ext, levels, src, len, hi, lo, batch, s)  \
+              : launch_swt_fused_t<ORDER, false, N>(t, ext, levels, src, len, hi, lo, batch, s);
+  switch (sigs) {
+    VS_SWT_SIGS(5) VS_SWT_SIGS(4) VS_SWT_SIGS(3) VS_SWT_SIGS(2)
+    default: break;
+  }
+  switch (1) { VS_SWT_SIGS(1) }
+  return VS_ERR_INVALID;
+#undef VS_SWT_SIGS
 }
 
 // Signals longer than one workgroup's LDS (len > kMultiMax): tiles of
@@ -478,6 +510,7 @@ vs_status launch_swt_tiled(const Taps &t, int ext, int levels, const float *src,
 // hi stores (+3 % on db8 x 8 levels: the hi rows are never re-read here).
 thread_local int g_swt_fused = 1;
 thread_local int g_swt_nt = 1;
+thread_local int g_swt_sigs = 2;
 // "dwt_vec" 1 (default) = vectorised pyramid kernel (dwt_multi4_kernel),
 // 0 = the scalar kernel.
 thread_local int g_dwt_vec = 1;
@@ -915,6 +948,10 @@ bool tune(const char *key, int value) {
     g_swt_fused = value < 0 ? 1 : value;
     return true;
   }
+  if (std::strcmp(key, "swt_sigs") == 0) {
+    g_swt_sigs = value < 0 ? 2 : value;
+    return true;
+  }
   if (std::strcmp(key, "swt_nt") == 0) {
     g_swt_nt = value < 0 ? 1 : value;
     return true;
@@ -943,6 +980,7 @@ bool tune(const char *key, int value) {
 void tune_reset() {
   g_swt_fused = 1;
   g_swt_nt = 1;
+  g_swt_sigs = 2;
   g_dwt_vec = 1;
   g_dwt_threads = 0;
   g_dwt_tile = kDwtTile;
