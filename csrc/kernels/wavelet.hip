@@ -166,7 +166,7 @@ constexpr int kMultiExt = 4096;   // room for the extension (order-1) 2^(L-1)
 
 __global__ __launch_bounds__(256) void swt_multi_kernel(
     Taps taps, int ext, int levels, const float *__restrict__ src, int len,
-    float *__restrict__ hi, float *__restrict__ lo) {
+    float *__restrict__ hi, int64_t hs, float *__restrict__ lo, int64_t ls) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int stride = len + ((taps.order - 1) << (levels - 1));
   float *band0 = smem, *band1 = smem + stride;
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void swt_multi_kernel(
       in[len + t] = j < 0 ? 0.f : in[j];
     }
     __syncthreads();
-    float *hrow = hi + (sig * levels + l) * len;
+    float *hrow = hi + sig * hs + static_cast<int64_t>(l) * len;
     for (int i = threadIdx.x; i < len; i += blockDim.x) {
       float sh = 0.f, sl = 0.f;
       for (int r = 0; r < taps.order; r++) {
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void swt_multi_kernel(
     out = t;
   }
   __syncthreads();
-  float *lrow = lo + sig * len;
+  float *lrow = lo + sig * ls;
   for (int i = threadIdx.x; i < len; i += blockDim.x) lrow[i] = in[i];
 }
 
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void swt_multi_kernel(
 template <int ORDER, bool NT, int SIGS>
 __global__ __launch_bounds__(256) void swt_fused_kernel(
     Taps taps, int ext, int levels, const float *__restrict__ src, int len,
-    float *__restrict__ hi, float *__restrict__ lo, int batch) {
+    float *__restrict__ hi, int64_t hs, float *__restrict__ lo, int64_t ls, int batch) {
   // SIGS signals per workgroup, interleaved lane by lane: every lane carries
   // SIGS independent float4 chains through each level and the level barrier
   // is shared.
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(256) void swt_fused_kernel(
         }
         const float4 hv = make_float4(sh[0], sh[1], sh[2], sh[3]);
         const float4 lv = make_float4(sl[0], sl[1], sl[2], sl[3]);
-        float4 *hrow = reinterpret_cast<float4 *>(hi + (sig * levels + l) * len);
+        float4 *hrow = reinterpret_cast<float4 *>(hi + sig * hs + static_cast<int64_t>(l) * len);
         if (NT) {
           typedef float native4 __attribute__((ext_vector_type(4)));
           const native4 nv = {hv.x, hv.y, hv.z, hv.w};
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256) void swt_fused_kernel(
           hrow[q] = hv;
         }
         if (last)
-          reinterpret_cast<float4 *>(lo + sig * len)[q] = lv;
+          reinterpret_cast<float4 *>(lo + sig * ls)[q] = lv;
         else
           put(out, i0, lv, next_halo);
       }
@@ -357,7 +357,8 @@ extern thread_local int g_swt_sigs;
 
 template <int ORDER, bool NT, int SIGS>
 vs_status launch_swt_fused_t(const Taps &t, int ext, int levels, const float *src, int len,
-                             float *hi, float *lo, int batch, hipStream_t s) {
+                             float *hi, int64_t hs, float *lo, int64_t ls, int batch,
+                             hipStream_t s) {
   const int halo = (ORDER - 1) << (levels - 1);
   const size_t lds =
       2 * SIGS * static_cast<size_t>((len + halo + 2 * ORDER + 8 + 3) & ~3) * sizeof(float);
@@ -367,14 +368,15 @@ vs_status launch_swt_fused_t(const Taps &t, int ext, int levels, const float *sr
   VS_HIP(attr);
   hipLaunchKernelGGL((swt_fused_kernel<ORDER, NT, SIGS>),
                      dim3(static_cast<unsigned>((batch + SIGS - 1) / SIGS)), dim3(256), lds, s, t,
-                     ext, levels, src, len, hi, lo, batch);
+                     ext, levels, src, len, hi, hs, lo, ls, batch);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
 
 template <int ORDER>
 vs_status launch_swt_fused(const Taps &t, int ext, int levels, const float *src, int len,
-                           float *hi, float *lo, int batch, bool nt, hipStream_t s) {
+                           float *hi, int64_t hs, float *lo, int64_t ls, int batch, bool nt,
+                           hipStream_t s) {
   const int halo = (ORDER - 1) << (levels - 1);
   const size_t one = 2 * static_cast<size_t>((len + halo + 2 * ORDER + 8 + 3) & ~3) * sizeof(float);
   // several signals per workgroup while their bands fit the CU's LDS
@@ -382,8 +384,10 @@ vs_status launch_swt_fused(const Taps &t, int ext, int levels, const float *src,
   while (sigs > 1 && sigs * one > 150 * 1024) sigs--;
 #define VS_SWT_SIGS(N)                                                                          \
   case N:                                                                                       \
-    return nt ? launch_swt_fused_t<ORDER, true, N>(t, ext, levels, src, len, hi, lo, batch, s)  \
-              : launch_swt_fused_t<ORDER, false, N>(t, ext, levels, src, len, hi, lo, batch, s);
+    return nt ? launch_swt_fused_t<ORDER, true, N>(t, ext, levels, src, len, hi, hs, lo, ls,   \
+                                                   batch, s)                                    \
+              : launch_swt_fused_t<ORDER, false, N>(t, ext, levels, src, len, hi, hs, lo, ls,  \
+                                                    batch, s);
   switch (sigs) {
     VS_SWT_SIGS(5) VS_SWT_SIGS(4) VS_SWT_SIGS(3) VS_SWT_SIGS(2)
     default: break;
@@ -409,7 +413,7 @@ constexpr int kTileOut = 4096;
 template <int ORDER>
 __global__ __launch_bounds__(256) void swt_tiled_kernel(
     Taps taps, int ext, int levels, const float *__restrict__ src, int64_t len,
-    float *__restrict__ hi, float *__restrict__ lo) {
+    float *__restrict__ hi, int64_t hs, float *__restrict__ lo, int64_t ls) {
   extern __shared__ __attribute__((aligned(16))) float smemt[];
   const int H = (ORDER - 1) * ((1 << levels) - 1);
   const int stride = (kTileOut + H + 2 * ORDER + 16 + 3) & ~3;
@@ -435,7 +439,7 @@ __global__ __launch_bounds__(256) void swt_tiled_kernel(
     const int dil = 1 << l;
     const int nout = (kTileOut + (ORDER - 1) * ((1 << levels) - (2 << l)) + 3) & ~3;
     __syncthreads();
-    float4 *hrow = reinterpret_cast<float4 *>(hi + (sig * levels + l) * len + t0);
+    float4 *hrow = reinterpret_cast<float4 *>(hi + sig * hs + l * len + t0);
     const bool last = l == levels - 1;
     for (int q = threadIdx.x; q < nout / 4; q += blockDim.x) {
       const int i0 = 4 * q;
@@ -464,7 +468,7 @@ __global__ __launch_bounds__(256) void swt_tiled_kernel(
         typedef float native4 __attribute__((ext_vector_type(4)));
         const native4 nv = {sh[0], sh[1], sh[2], sh[3]};
         __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(hrow + q));
-        if (last) reinterpret_cast<float4 *>(lo + sig * len + t0)[q] = lv;
+        if (last) reinterpret_cast<float4 *>(lo + sig * ls + t0)[q] = lv;
       }
       if (!last) reinterpret_cast<float4 *>(out)[q] = lv;
     }
@@ -488,7 +492,8 @@ __global__ __launch_bounds__(256) void swt_tiled_kernel(
 
 template <int ORDER>
 vs_status launch_swt_tiled(const Taps &t, int ext, int levels, const float *src, int64_t len,
-                           float *hi, float *lo, int batch, hipStream_t s) {
+                           float *hi, int64_t hs, float *lo, int64_t ls, int batch,
+                           hipStream_t s) {
   const int H = (ORDER - 1) * ((1 << levels) - 1);
   const size_t lds = 2 * static_cast<size_t>((kTileOut + H + 2 * ORDER + 16 + 3) & ~3) * 4;
   static const hipError_t attr = hipFuncSetAttribute(
@@ -499,7 +504,7 @@ vs_status launch_swt_tiled(const Taps &t, int ext, int levels, const float *src,
   const dim3 grid(static_cast<unsigned>((len + kTileOut - 1) / kTileOut),
                   static_cast<unsigned>(batch));
   hipLaunchKernelGGL(swt_tiled_kernel<ORDER>, grid, dim3(256), lds, s, t, ext, levels, src,
-                     len, hi, lo);
+                     len, hi, hs, lo, ls);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
@@ -1052,9 +1057,13 @@ vs_status vs_swt(int type, int order, int level, int ext, const float *src,
                     static_cast<hipStream_t>(stream));
 }
 
-vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
-                            const float *src, int64_t len64, float *hi, float *lo,
-                            int batch, vs_stream_t stream) {
+}  // extern "C"
+
+// hi rows of signal b at hi + b hs (level l at + l len), its low band at
+// lo + b ls.
+static vs_status swt_multilevel(int type, int order, int levels, int ext, const float *src,
+                                int64_t len64, float *hi, int64_t hs, float *lo, int64_t ls,
+                                int batch, vs_stream_t stream) {
   // whole-signal kernels (len <= kMultiMax) index with int; the tiled and
   // level-by-level paths take the 64-bit length
   const int len = static_cast<int>(std::min<int64_t>(len64, INT32_MAX));
@@ -1071,7 +1080,7 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
     const bool nt = g_swt_nt != 0;
     switch (order) {
 #define VS_SWTF(O) \
-  case O: return launch_swt_fused<O>(t, ext, levels, src, len, hi, lo, batch, nt, s);
+  case O: return launch_swt_fused<O>(t, ext, levels, src, len, hi, hs, lo, ls, batch, nt, s);
       VS_SWTF(2) VS_SWTF(4) VS_SWTF(6) VS_SWTF(8) VS_SWTF(10) VS_SWTF(12) VS_SWTF(14)
       VS_SWTF(16) VS_SWTF(18) VS_SWTF(20) VS_SWTF(24) VS_SWTF(30)
 #undef VS_SWTF
@@ -1085,7 +1094,7 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (kMultiMax + kMultiExt) * 4);
     VS_HIP(attr);
     hipLaunchKernelGGL(swt_multi_kernel, dim3(static_cast<unsigned>(batch)),
-                       dim3(256), lds, s, t, ext, levels, src, len, hi, lo);
+                       dim3(256), lds, s, t, ext, levels, src, len, hi, hs, lo, ls);
     VS_HIP(hipGetLastError());
     return VS_OK;
   }
@@ -1095,7 +1104,7 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
       g_swt_fused) {
     switch (order) {
 #define VS_SWTT(O) \
-  case O: return launch_swt_tiled<O>(t, ext, levels, src, len64, hi, lo, batch, s);
+  case O: return launch_swt_tiled<O>(t, ext, levels, src, len64, hi, hs, lo, ls, batch, s);
       VS_SWTT(2) VS_SWTT(4) VS_SWTT(6) VS_SWTT(8) VS_SWTT(10) VS_SWTT(12) VS_SWTT(14)
       VS_SWTT(16) VS_SWTT(18) VS_SWTT(20) VS_SWTT(24) VS_SWTT(30)
 #undef VS_SWTT
@@ -1106,20 +1115,38 @@ vs_status vs_swt_multilevel(int type, int order, int levels, int ext,
   // ping-ponging between two scratch bands; the last level writes lo).
   if (batch > kMaxGridY)
     return batch_chunks(batch, [&](long long b0, int nb) {
-      return vs_swt_multilevel(type, order, levels, ext, src + b0 * len64, len64,
-                               hi + b0 * levels * len64, lo + b0 * len64, nb, stream);
+      return swt_multilevel(type, order, levels, ext, src + b0 * len64, len64, hi + b0 * hs, hs,
+                            lo + b0 * ls, ls, nb, stream);
     });
   DeviceBuffer tmp;
   const size_t band = static_cast<size_t>(len64) * batch;
   VS_TRY(tmp.alloc(2 * band * sizeof(float), s));
   const float *in = src;
+  int64_t in_stride = len64;
   for (int l = 1; l <= levels; l++) {
-    float *dst = l == levels ? lo : tmp.as<float>() + (l % 2) * band;
-    VS_TRY(launch_swt(t, l, ext, in, len64, len64, hi + (l - 1) * len64, levels * len64, dst,
-                      len64, batch, s));
+    const bool last = l == levels;
+    float *dst = last ? lo : tmp.as<float>() + (l % 2) * band;
+    VS_TRY(launch_swt(t, l, ext, in, len64, l == 1 ? len64 : in_stride, hi + (l - 1) * len64, hs,
+                      dst, last ? ls : len64, batch, s));
     in = dst;
+    in_stride = last ? ls : len64;
   }
   return VS_OK;
+}
+
+extern "C" {
+
+vs_status vs_swt_multilevel(int type, int order, int levels, int ext, const float *src,
+                            int64_t len, float *hi, float *lo, int batch, vs_stream_t stream) {
+  return swt_multilevel(type, order, levels, ext, src, len, hi, levels * len, lo, len, batch,
+                        stream);
+}
+
+vs_status vs_swt_multilevel_packed(int type, int order, int levels, int ext, const float *src,
+                                   int64_t len, float *out, int batch, vs_stream_t stream) {
+  VS_REQUIRE(out, "vs_swt_multilevel_packed: null pointer");
+  return swt_multilevel(type, order, levels, ext, src, len, out, (levels + 1) * len,
+                        out + levels * len, (levels + 1) * len, batch, stream);
 }
 
 vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,

@@ -44,6 +44,9 @@ def main():
     x = torch.randn(nsig, n, device="cuda")
     hi = torch.empty(nsig, levels, n, device="cuda")
     lo = torch.empty(nsig, n, device="cuda")
+    packed = torch.empty(nsig, levels + 1, n, device="cuda") if os.environ.get("PACKED") == "1" else None
+    if packed is not None:
+        hi, lo = packed[:, :levels], packed[:, levels]
     nbytes = 4 * nsig * n * (levels + 2)
     res = {}
     # ceilings on the same volume (NO_CEIL=1 skips them)
@@ -63,9 +66,14 @@ def main():
                 lib.vs_tune_set(k.encode(), v)
 
             def run():
-                st = lib.vs_swt_multilevel(0, order, levels, 0, ctypes.c_void_p(x.data_ptr()), n,
-                                           ctypes.c_void_p(hi.data_ptr()),
-                                           ctypes.c_void_p(lo.data_ptr()), nsig, s)
+                if os.environ.get("PACKED") == "1":   # one [signals][levels + 1][len] array
+                    st = lib.vs_swt_multilevel_packed(0, order, levels, 0,
+                                                      ctypes.c_void_p(x.data_ptr()), n,
+                                                      ctypes.c_void_p(packed.data_ptr()), nsig, s)
+                else:
+                    st = lib.vs_swt_multilevel(0, order, levels, 0, ctypes.c_void_p(x.data_ptr()),
+                                               n, ctypes.c_void_p(hi.data_ptr()),
+                                               ctypes.c_void_p(lo.data_ptr()), nsig, s)
                 assert st == 0, lib.vs_last_error()
             run()
             torch.cuda.synchronize()

@@ -99,6 +99,7 @@ _SIGNATURES = {
     "vs_dwt": (_i, [_i, _i, _i, _vp, _i64, _i64, _vp, _vp, _i64, _i, _vp]),
     "vs_swt": (_i, [_i, _i, _i, _i, _vp, _i64, _i64, _vp, _vp, _i64, _i, _vp]),
     "vs_swt_multilevel": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _i, _vp]),
+    "vs_swt_multilevel_packed": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i, _vp]),
     "vs_dwt_multilevel": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i, _vp]),
     "vs_wavelet_filter": (_i, [_i, _i, _vp]),
     "vs_detect_peaks": (_i, [_vp, _sz, _i, _vp, _vp, _sz, _vp, _vp]),

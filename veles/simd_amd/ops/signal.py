@@ -355,14 +355,12 @@ def _swt(x: torch.Tensor, family: int, order: int, levels: int,
         out = torch.cat([torch.stack(his, 1), cur[:, None]], 1).float()
         return out.reshape(*lead, levels + 1, n)
     require_gpu_tensor(x, "veles::swt")
+    # one allocation, rows 0..levels-1 = hi, row levels = lo: the kernels
+    # write both straight into it (a signal's rows are contiguous)
     out = torch.empty((batch, levels + 1, n), dtype=torch.float32, device=x.device)
-    hi = torch.empty((batch, levels, n), dtype=torch.float32, device=x.device)
-    lo = torch.empty((batch, n), dtype=torch.float32, device=x.device)
     with on_device(x):
-        _lib.call("vs_swt_multilevel", family, order, levels, ext, ptr(xr), n,
-                  ptr(hi), ptr(lo), batch, stream_of(x))
-    out[:, :levels] = hi
-    out[:, levels] = lo
+        _lib.call("vs_swt_multilevel_packed", family, order, levels, ext, ptr(xr), n,
+                  ptr(out), batch, stream_of(x))
     return out.reshape(*lead, levels + 1, n)
 
 
