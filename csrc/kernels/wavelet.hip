@@ -267,8 +267,17 @@ __global__ __launch_bounds__(256) void swt_fused_kernel(
   for (int g = 0; g < SIGS; g++) {
     const float4 *x4 =
         reinterpret_cast<const float4 *>(src + min(sig0 + g, sig_last) * len);
-    for (int q = threadIdx.x; q < len4; q += blockDim.x)
-      put(smemf + 2 * g * stride, 4 * q, x4[q], ORDER - 1);
+    for (int q = threadIdx.x; q < len4; q += blockDim.x) {
+      float4 v;
+      if (NT) {  // read once: keep it out of the caches the stores stream through
+        typedef float native4 __attribute__((ext_vector_type(4)));
+        const native4 nv = __builtin_nontemporal_load(reinterpret_cast<const native4 *>(x4) + q);
+        v = make_float4(nv.x, nv.y, nv.z, nv.w);
+      } else {
+        v = x4[q];
+      }
+      put(smemf + 2 * g * stride, 4 * q, v, ORDER - 1);
+    }
   }
   int par = 0;
   for (int l = 0; l < levels; l++) {
