@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "csrc/kernels/device.h"
 #include "csrc/runtime/runtime.h"
@@ -25,6 +26,16 @@ constexpr unsigned kBlock = 256;
 
 inline bool aligned_to(const void *p, size_t a) {
   return (reinterpret_cast<uintptr_t>(p) % a) == 0;
+}
+
+// VELES_STREAM_NT=0 turns the non-temporal path of the streaming kernels off
+// (A/B measurements).
+inline bool stream_nt() {
+  static const bool on = [] {
+    const char *e = std::getenv("VELES_STREAM_NT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // ------------------------------------------------------------ conversions
@@ -79,18 +90,22 @@ struct Convert<float, float> {
   __device__ float operator()(float v) const { return v; }
 };
 
-template <class In, class Out, class F, int V>
+// NT: arrays too large for the caches to matter stream through with
+// non-temporal loads and stores (kStreamBytes).
+constexpr size_t kStreamBytes = static_cast<size_t>(64) << 20;
+
+template <class In, class Out, class F, int V, bool NT>
 __global__ __launch_bounds__(kBlock) void map1_kernel(
     const In *__restrict__ in, Out *__restrict__ out, size_t n, F f) {
   const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   const size_t nv = n / V;
   for (size_t i = tid; i < nv; i += stride) {
-    Vec<In, V> a = reinterpret_cast<const Vec<In, V> *>(in)[i];
+    const Vec<In, V> a = dev::load_vec<NT>(reinterpret_cast<const Vec<In, V> *>(in) + i);
     Vec<Out, V> r;
 #pragma unroll
     for (int j = 0; j < V; j++) r.v[j] = f(a.v[j]);
-    reinterpret_cast<Vec<Out, V> *>(out)[i] = r;
+    dev::store_vec<NT>(reinterpret_cast<Vec<Out, V> *>(out) + i, r);
   }
   for (size_t i = nv * V + tid; i < n; i += stride) out[i] = f(in[i]);
 }
@@ -102,17 +117,20 @@ vs_status launch_map1(const In *in, Out *out, size_t n, F f,
   constexpr int V = 4;
   const bool vec = aligned_to(in, sizeof(In) * V) && aligned_to(out, sizeof(Out) * V);
   const unsigned grid = elementwise_grid(vec ? (n + V - 1) / V : n, kBlock);
-  if (vec)
-    hipLaunchKernelGGL((map1_kernel<In, Out, F, V>), dim3(grid), dim3(kBlock),
+  if (vec && n * (sizeof(In) + sizeof(Out)) >= kStreamBytes && stream_nt())
+    hipLaunchKernelGGL((map1_kernel<In, Out, F, V, true>), dim3(grid), dim3(kBlock),
+                       0, stream, in, out, n, f);
+  else if (vec)
+    hipLaunchKernelGGL((map1_kernel<In, Out, F, V, false>), dim3(grid), dim3(kBlock),
                        0, stream, in, out, n, f);
   else
-    hipLaunchKernelGGL((map1_kernel<In, Out, F, 1>), dim3(grid), dim3(kBlock),
+    hipLaunchKernelGGL((map1_kernel<In, Out, F, 1, false>), dim3(grid), dim3(kBlock),
                        0, stream, in, out, n, f);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
 
-template <class A, class B, class Out, class F, int V>
+template <class A, class B, class Out, class F, int V, bool NT>
 __global__ __launch_bounds__(kBlock) void map2_kernel(
     const A *__restrict__ a, const B *__restrict__ b, Out *__restrict__ out,
     size_t n, F f) {
@@ -120,12 +138,12 @@ __global__ __launch_bounds__(kBlock) void map2_kernel(
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   const size_t nv = n / V;
   for (size_t i = tid; i < nv; i += stride) {
-    Vec<A, V> x = reinterpret_cast<const Vec<A, V> *>(a)[i];
-    Vec<B, V> y = reinterpret_cast<const Vec<B, V> *>(b)[i];
+    const Vec<A, V> x = dev::load_vec<NT>(reinterpret_cast<const Vec<A, V> *>(a) + i);
+    const Vec<B, V> y = dev::load_vec<NT>(reinterpret_cast<const Vec<B, V> *>(b) + i);
     Vec<Out, V> r;
 #pragma unroll
     for (int j = 0; j < V; j++) r.v[j] = f(x.v[j], y.v[j]);
-    reinterpret_cast<Vec<Out, V> *>(out)[i] = r;
+    dev::store_vec<NT>(reinterpret_cast<Vec<Out, V> *>(out) + i, r);
   }
   for (size_t i = nv * V + tid; i < n; i += stride) out[i] = f(a[i], b[i]);
 }
@@ -138,11 +156,14 @@ vs_status launch_map2(const A *a, const B *b, Out *out, size_t n, F f,
   const bool vec = aligned_to(a, sizeof(A) * V) && aligned_to(b, sizeof(B) * V) &&
                    aligned_to(out, sizeof(Out) * V);
   const unsigned grid = elementwise_grid(vec ? (n + V - 1) / V : n, kBlock);
-  if (vec)
-    hipLaunchKernelGGL((map2_kernel<A, B, Out, F, V>), dim3(grid), dim3(kBlock),
+  if (vec && n * (sizeof(A) + sizeof(B) + sizeof(Out)) >= kStreamBytes && stream_nt())
+    hipLaunchKernelGGL((map2_kernel<A, B, Out, F, V, true>), dim3(grid), dim3(kBlock),
+                       0, stream, a, b, out, n, f);
+  else if (vec)
+    hipLaunchKernelGGL((map2_kernel<A, B, Out, F, V, false>), dim3(grid), dim3(kBlock),
                        0, stream, a, b, out, n, f);
   else
-    hipLaunchKernelGGL((map2_kernel<A, B, Out, F, 1>), dim3(grid), dim3(kBlock),
+    hipLaunchKernelGGL((map2_kernel<A, B, Out, F, 1, false>), dim3(grid), dim3(kBlock),
                        0, stream, a, b, out, n, f);
   VS_HIP(hipGetLastError());
   return VS_OK;
@@ -202,20 +223,40 @@ struct PowOp {
   }
 };
 
+// float4 access, non-temporal when `nt` (uniform): see kStreamBytes.
+__device__ __forceinline__ float4 ld4(const float4 *p, bool nt) {
+  typedef float native4 __attribute__((ext_vector_type(4)));
+  if (nt) {
+    const native4 r = __builtin_nontemporal_load(reinterpret_cast<const native4 *>(p));
+    return make_float4(r.x, r.y, r.z, r.w);
+  }
+  return *p;
+}
+__device__ __forceinline__ void st4(float4 *p, float4 v, bool nt) {
+  typedef float native4 __attribute__((ext_vector_type(4)));
+  if (nt) {
+    const native4 r = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(r, reinterpret_cast<native4 *>(p));
+  } else {
+    *p = v;
+  }
+}
+
 // sin and cos of the same argument: one shared range reduction per element
 // (OCML sincosf), two 16-byte stores per lane.
 __global__ __launch_bounds__(kBlock) void sincos_kernel(const float *__restrict__ x,
                                                         float *__restrict__ s,
-                                                        float *__restrict__ c, size_t n) {
+                                                        float *__restrict__ c, size_t n,
+                                                        bool nt) {
   const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   const size_t nv = n / 4;
   for (size_t i = tid; i < nv; i += stride) {
-    const float4 v = reinterpret_cast<const float4 *>(x)[i];
+    const float4 v = ld4(reinterpret_cast<const float4 *>(x) + i, nt);
     float4 sv, cv;
     simd_sincos_ps4(v, &sv, &cv);
-    reinterpret_cast<float4 *>(s)[i] = sv;
-    reinterpret_cast<float4 *>(c)[i] = cv;
+    st4(reinterpret_cast<float4 *>(s) + i, sv, nt);
+    st4(reinterpret_cast<float4 *>(c) + i, cv, nt);
   }
   for (size_t i = 4 * nv + tid; i < n; i += stride) simd_sincos_ps(x[i], s + i, c + i);
 }
@@ -233,21 +274,29 @@ __global__ __launch_bounds__(kBlock) void sincos_scalar_kernel(const float *__re
 template <bool CONJ, int V>
 __global__ __launch_bounds__(kBlock) void cmul_kernel(
     const float2 *__restrict__ a, const float2 *__restrict__ b,
-    float2 *__restrict__ out, size_t n) {
+    float2 *__restrict__ out, size_t n, bool nt) {
   const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   const size_t nv = n / V;
   for (size_t i = tid; i < nv; i += stride) {
-    Vec<float2, V> x = reinterpret_cast<const Vec<float2, V> *>(a)[i];
-    Vec<float2, V> y = reinterpret_cast<const Vec<float2, V> *>(b)[i];
-    Vec<float2, V> r;
+    Vec<float2, V> x, y, r;
+    if constexpr (V == 2) {
+      x = __builtin_bit_cast(Vec<float2, V>, ld4(reinterpret_cast<const float4 *>(a) + i, nt));
+      y = __builtin_bit_cast(Vec<float2, V>, ld4(reinterpret_cast<const float4 *>(b) + i, nt));
+    } else {
+      x = reinterpret_cast<const Vec<float2, V> *>(a)[i];
+      y = reinterpret_cast<const Vec<float2, V> *>(b)[i];
+    }
 #pragma unroll
     for (int j = 0; j < V; j++) {
       const float yi = CONJ ? -y.v[j].y : y.v[j].y;
       r.v[j].x = x.v[j].x * y.v[j].x - x.v[j].y * yi;
       r.v[j].y = x.v[j].x * yi + y.v[j].x * x.v[j].y;
     }
-    reinterpret_cast<Vec<float2, V> *>(out)[i] = r;
+    if constexpr (V == 2)
+      st4(reinterpret_cast<float4 *>(out) + i, __builtin_bit_cast(float4, r), nt);
+    else
+      reinterpret_cast<Vec<float2, V> *>(out)[i] = r;
   }
   for (size_t i = nv * V + tid; i < n; i += stride) {
     const float yi = CONJ ? -b[i].y : b[i].y;
@@ -263,17 +312,17 @@ __global__ __launch_bounds__(kBlock) void cmul_kernel(
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void conj_kernel(const float *__restrict__ a,
                                                       float *__restrict__ out,
-                                                      size_t n) {
+                                                      size_t n, bool nt) {
   const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   size_t done = 0;
   if (VEC) {
     const size_t n4 = n / 4;
     for (size_t i = tid; i < n4; i += stride) {
-      float4 v = reinterpret_cast<const float4 *>(a)[i];
+      float4 v = ld4(reinterpret_cast<const float4 *>(a) + i, nt);
       v.y = -v.y;
       v.w = -v.w;
-      reinterpret_cast<float4 *>(out)[i] = v;
+      st4(reinterpret_cast<float4 *>(out) + i, v, nt);
     }
     done = n4 * 4;
   }
@@ -297,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(float *__restrict__ p,
 
 template <bool PAIRS, bool VEC = false>
 __global__ __launch_bounds__(kBlock) void reverse_kernel(
-    const float *__restrict__ src, float *__restrict__ dst, size_t n) {
+    const float *__restrict__ src, float *__restrict__ dst, size_t n, bool nt) {
   const size_t tid = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x;
   const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
   if (PAIRS) {
@@ -312,8 +361,8 @@ __global__ __launch_bounds__(kBlock) void reverse_kernel(
     const size_t n4 = n / 4;
     const float4 *s4 = reinterpret_cast<const float4 *>(src + n) - 1;
     for (size_t i = tid; i < n4; i += stride) {
-      const float4 v = *(s4 - i);
-      reinterpret_cast<float4 *>(dst)[i] = make_float4(v.w, v.z, v.y, v.x);
+      const float4 v = ld4(s4 - i, nt);
+      st4(reinterpret_cast<float4 *>(dst) + i, make_float4(v.w, v.z, v.y, v.x), nt);
     }
     for (size_t i = 4 * n4 + tid; i < n; i += stride) dst[i] = src[n - 1 - i];
   } else {
@@ -376,16 +425,17 @@ vs_status vs_complex_multiply(const float *a, const float *b, float *out,
   auto co = reinterpret_cast<float2 *>(out);
   const bool vec = aligned_to(a, 16) && aligned_to(b, 16) && aligned_to(out, 16);
   const unsigned grid = elementwise_grid(vec ? n / 2 + 1 : n, kBlock);
+  const bool nt = n * 24 >= kStreamBytes && stream_nt();
   if (conjugate_b) {
     if (vec)
-      hipLaunchKernelGGL((cmul_kernel<true, 2>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+      hipLaunchKernelGGL((cmul_kernel<true, 2>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n, nt);
     else
-      hipLaunchKernelGGL((cmul_kernel<true, 1>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+      hipLaunchKernelGGL((cmul_kernel<true, 1>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n, nt);
   } else {
     if (vec)
-      hipLaunchKernelGGL((cmul_kernel<false, 2>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+      hipLaunchKernelGGL((cmul_kernel<false, 2>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n, nt);
     else
-      hipLaunchKernelGGL((cmul_kernel<false, 1>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n);
+      hipLaunchKernelGGL((cmul_kernel<false, 1>), dim3(grid), dim3(kBlock), 0, s, ca, cb, co, n, nt);
   }
   VS_HIP(hipGetLastError());
   return VS_OK;
@@ -402,10 +452,11 @@ vs_status vs_complex_conjugate(const float *a, float *out, size_t n,
   // one float4 per lane (3.6 -> ~5.8 TB/s at 2^26, tools/bench_memops.py)
   if (aligned_to(a, 16) && aligned_to(out, 16))
     hipLaunchKernelGGL(conj_kernel<true>, dim3(elementwise_grid(even / 4 + 1, kBlock)),
-                       dim3(kBlock), 0, static_cast<hipStream_t>(stream), a, out, even);
+                       dim3(kBlock), 0, static_cast<hipStream_t>(stream), a, out, even,
+                       even * 8 >= kStreamBytes && stream_nt());
   else
     hipLaunchKernelGGL(conj_kernel<false>, dim3(elementwise_grid(even, kBlock)),
-                       dim3(kBlock), 0, static_cast<hipStream_t>(stream), a, out, even);
+                       dim3(kBlock), 0, static_cast<hipStream_t>(stream), a, out, even, false);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
@@ -446,13 +497,13 @@ vs_status vs_reverse(const float *src, float *dst, size_t n, int pairs,
   auto s = static_cast<hipStream_t>(stream);
   if (pairs)
     hipLaunchKernelGGL(reverse_kernel<true>, dim3(elementwise_grid(n / 2, kBlock)),
-                       dim3(kBlock), 0, s, src, dst, n);
+                       dim3(kBlock), 0, s, src, dst, n, false);
   else if (aligned_to(dst, 16) && aligned_to(src + n, 16))
     hipLaunchKernelGGL((reverse_kernel<false, true>), dim3(elementwise_grid(n / 4 + 1, kBlock)),
-                       dim3(kBlock), 0, s, src, dst, n);
+                       dim3(kBlock), 0, s, src, dst, n, n * 8 >= kStreamBytes && stream_nt());
   else
     hipLaunchKernelGGL(reverse_kernel<false>, dim3(elementwise_grid(n, kBlock)),
-                       dim3(kBlock), 0, s, src, dst, n);
+                       dim3(kBlock), 0, s, src, dst, n, false);
   VS_HIP(hipGetLastError());
   return VS_OK;
 }
@@ -495,7 +546,7 @@ vs_status vs_sincos(const float *x, float *s, float *c, size_t n, vs_stream_t st
   const auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (al(x) && al(s) && al(c))
     hipLaunchKernelGGL(sincos_kernel, dim3(elementwise_grid((n + 3) / 4, kBlock)), dim3(kBlock),
-                       0, st, x, s, c, n);
+                       0, st, x, s, c, n, n * 12 >= kStreamBytes && stream_nt());
   else
     hipLaunchKernelGGL(sincos_scalar_kernel, dim3(elementwise_grid(n, kBlock)), dim3(kBlock), 0,
                        st, x, s, c, n);

@@ -42,6 +42,9 @@ KNOBS = [
     Knob("VELES_SCRATCH_CACHE_MB", "8192", "cap of the device scratch cache (freed blocks "
          "kept for reuse, per stream); above it the oldest blocks are released",
          "csrc/runtime/runtime.cpp"),
+    Knob("VELES_STREAM_NT", "1", "0: plain instead of non-temporal loads / stores in the "
+         "elementwise kernels on arrays past 64 MB (A/B measurements)",
+         "csrc/kernels/elementwise.hip"),
     Knob("VELES_GEMM_BF16_VARIANT", "-1", "force a bf16 GEMM variant (0: 128 tiles, "
          "1: large tiles)", "csrc/kernels/gemm_bf16.hip"),
     Knob("VELES_GEMM_BF16_PACK", "-1", "force (1) or forbid (0) the bf16 operand pre-pack "
