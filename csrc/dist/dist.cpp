@@ -223,7 +223,8 @@ vs_status halo_on(vs_dist_context *c, const std::vector<hipStream_t> &s,
   for (int r = 0; r < n; r++)
     if (peer[r] < 0) {
       DevGuard g(c->dev[r]);
-      VS_HIP(hipMemsetAsync(halo[r], 0, bytes, s[r]));
+      // a fill kernel, not a memset: callers may capture the stream
+      VS_TRY(vs_fill(halo[r], 0.f, h, s[r]));
     }
   if (c->backend == VS_DIST_RCCL) {
     // self-exchange (periodic, one rank) is a local copy

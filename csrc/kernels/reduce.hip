@@ -287,8 +287,7 @@ vs_status vs_sum(const float *x, size_t n, float *out, vs_stream_t stream) {
   VS_REQUIRE(x && out, "vs_sum: null pointer");
   auto s = static_cast<hipStream_t>(stream);
   if (n == 0) {
-    VS_HIP(hipMemsetAsync(out, 0, sizeof(float), s));
-    return VS_OK;
+    return vs_fill(out, 0.f, 1, stream);  // a kernel, not a memset: the stream may be captured
   }
   const unsigned g = partial_count(n);
   DeviceBuffer part;
