@@ -304,6 +304,15 @@ __global__ __launch_bounds__(256) void pad_filter_kernel(
 }
 
 // ------------------------------------------------ fused block convolution
+// Cache policy of the block kernels' output stores (aux operand of the
+// buffer stores: bit 1 = non-temporal).  The outputs are written once and
+// never re-read by the kernel; kept out of L2 they stop evicting the block
+// overlaps, P / Q tables and twiddles the workgroups share: 2^20 x 4096 x 64
+// went from 303 to 334 K Msamples/s per call and from 327 to 366 K through a
+// plan.  Non-temporal input loads gained 1 % alone and cost 6 % on top of
+// the stores (profiles/r3/conv/nt_stores.md).
+constexpr int kConvStoreAux = 2;
+
 struct BlockArgs {
   const float *x;
   int64_t xs;
@@ -425,9 +434,9 @@ __device__ __forceinline__ void store_pair(const BlockArgs &a, const PairPos &q,
         if (n < 0 || n >= a.step) continue;
         const float2 r = v[b * RI + j];
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.x * a.scale), w0,
-                                              4 * (base0 + a.pre + n), 0, 0);
+                                              4 * (base0 + a.pre + n), 0, kConvStoreAux);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r.y * a.scale), w1,
-                                              4 * (base1 + a.pre + n), 0, 0);
+                                              4 * (base1 + a.pre + n), 0, kConvStoreAux);
       }
   } else {
 #pragma unroll
@@ -439,8 +448,8 @@ __device__ __forceinline__ void store_pair(const BlockArgs &a, const PairPos &q,
         const float2 r = v[b * RI + j];
         const long long o0 = static_cast<long long>(q.b0) * a.step + n;
         const long long o1 = static_cast<long long>(q.b1) * a.step + n;
-        if (q.ok0 && o0 < a.ylen) y0[o0] = r.x * a.scale;
-        if (q.ok1 && o1 < a.ylen) y1[o1] = r.y * a.scale;
+        if (q.ok0 && o0 < a.ylen) __builtin_nontemporal_store(r.x * a.scale, y0 + o0);
+        if (q.ok1 && o1 < a.ylen) __builtin_nontemporal_store(r.y * a.scale, y1 + o1);
       }
   }
 }
@@ -584,7 +593,7 @@ __device__ __forceinline__ void store_real(const RealArgs &a, float *yr, int st,
         }
         __attribute__((ext_vector_type(2))) unsigned u = {__float_as_uint(r.x),
                                                            __float_as_uint(r.y)};
-        __builtin_amdgcn_raw_buffer_store_b64(u, w, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(u, w, off, 0, kConvStoreAux);
       }
   } else {
 #pragma unroll
@@ -595,8 +604,8 @@ __device__ __forceinline__ void store_real(const RealArgs &a, float *yr, int st,
         const float2 r = v[b * R0 + j];
         const bool ok0 = p >= lo && p < hi, ok1 = p + 1 >= lo && p + 1 < hi;
         float *dst = yr + st + p;
-        if (ok0) dst[0] = a.accumulate ? dst[0] + r.x : r.x;
-        if (ok1) dst[1] = a.accumulate ? dst[1] + r.y : r.y;
+        if (ok0) __builtin_nontemporal_store(a.accumulate ? dst[0] + r.x : r.x, dst);
+        if (ok1) __builtin_nontemporal_store(a.accumulate ? dst[1] + r.y : r.y, dst + 1);
       }
   }
 }

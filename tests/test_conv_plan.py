@@ -17,7 +17,7 @@ def _ref(x, h, algo, corr):
     (9000, 3000, 2, False, "fft", True),             # one real block
     (200000, 20000, 1, False, "auto", True),         # L = 32768 blocks (15 % rule)
     (5000, 16, 4, False, "auto", False),             # direct: taps copied, vs_conv1d
-    (200000, 40000, 1, False, "overlap_save", False),  # partitioned: vs_conv1d
+    (200000, 40000, 1, False, "overlap_save", True),   # partitioned: one P / Q table per partition
 ])
 @pytest.mark.parametrize("corr", [False, True])
 def test_plan_matches_conv1d(xlen, hlen, batch, per_signal, algo, precomputed, corr):

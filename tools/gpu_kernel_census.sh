@@ -2,7 +2,7 @@
 # Kernel census of the GPU test suite: first the
 # reference-shape device tests alone, then `pytest -m gpu` under
 # rocprofv3 --kernel-trace --stats; tools/kernel_census.py turns the stats
-# into profiles/r2/gpu_suite_kernels.md.
+# into a markdown table (profiles/*/gpu_suite_kernels.md).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"

@@ -19,10 +19,10 @@ ROWS = [
     ("K5 reductions", r"sum_pass|minmax_pass"),
     ("K6 normalize2D", r"normalize2d|minmax2d"),
     ("K7 mathfun", r"MathOp|sincos|PowOp"),
-    ("K8 SGEMM / GEMM", r"sgemm|gemm_glds|scale_c|pack_kernel"),
+    ("K8 SGEMM / GEMM", r"sgemm|gemm_glds|scale_c|pack_kernel|slices_reduce"),
     ("K9 direct conv", r"direct"),
     ("K10 FFT", r"fft::"),
-    ("K11 fused overlap-save / block conv", r"block_conv|real_conv|real_filter"),
+    ("K11 fused overlap-save / block conv", r"block_conv|real_conv|real_filter|fdl_"),
     ("K12 fused pointwise", r"spectrum_mul|pack_pairs|unpack_pairs|pad_filter"),
     ("K13 DWT", r"dwt"),
     ("K14 SWT", r"swt"),
