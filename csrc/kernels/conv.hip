@@ -68,7 +68,9 @@ __device__ __forceinline__ void store_outputs(const float (&acc)[kDirPerThread],
 #pragma unroll
   for (int k = 0; k < kDirPerThread; k++) {
     const int i = threadIdx.x + k * kDirThreads;
-    if (n0 + i < ylen) yrow[n0 + i] = buf[i];
+    // written once, never re-read here: non-temporal (h = 64 direct: 320 -> 437 K
+    // Msamples/s at 2^20 x 64, h = 4: 600 -> 662 K; profiles/r3/conv/nt_sites_ab.log)
+    if (n0 + i < ylen) __builtin_nontemporal_store(buf[i], yrow + n0 + i);
   }
 }
 
@@ -212,7 +214,9 @@ __global__ __launch_bounds__(kDirThreads) void direct_small_kernel(
       const int b = d + 4 * g;
       const float4 v = make_float4(sx[b], sx[b + 1], sx[b + 2], sx[b + 3]);
       if (o + 3 < ylen) {
-        *reinterpret_cast<float4 *>(yrow + o) = v;
+        typedef float native4 __attribute__((ext_vector_type(4)));
+        const native4 nv = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(yrow + o));
       } else {
         if (o < ylen) yrow[o] = v.x;
         if (o + 1 < ylen) yrow[o + 1] = v.y;
@@ -856,7 +860,11 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())
 #pragma unroll
   for (int b = 0; b < E / RL; b++)
 #pragma unroll
-    for (int j = 0; j < RL; j++) z[reg_index<PL, RL>(t, b, j)] = v[b * RL + j];
+    for (int j = 0; j < RL; j++) {
+      typedef float native2 __attribute__((ext_vector_type(2)));
+      const native2 nv = {v[b * RL + j].x, v[b * RL + j].y};
+      __builtin_nontemporal_store(nv, reinterpret_cast<native2 *>(z + reg_index<PL, RL>(t, b, j)));
+    }
 }
 
 template <int LOGM, int EP, bool BUF>
@@ -946,8 +954,11 @@ __global__ __launch_bounds__(256) void fdl_mac_kernel(FdlMac a) {
 #pragma unroll
   for (int o = 0; o < kFdlTile; o++) {
     if (b0 + o >= a.nblk) break;
-    Y[static_cast<long long>(b0 + o) * a.m + k] = acck[o];
-    Y[static_cast<long long>(b0 + o) * a.m + km] = accm[o];
+    typedef float native2 __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(native2{acck[o].x, acck[o].y},
+                                reinterpret_cast<native2 *>(Y + static_cast<long long>(b0 + o) * a.m + k));
+    __builtin_nontemporal_store(native2{accm[o].x, accm[o].y},
+                                reinterpret_cast<native2 *>(Y + static_cast<long long>(b0 + o) * a.m + km));
   }
 }
 

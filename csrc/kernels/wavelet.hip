@@ -683,7 +683,11 @@ __global__ __launch_bounds__(256) void dwt_multi4_kernel(
             sh[e] = fmaf(hp[j], w[2 * e + j], sh[e]);
             sl[e] = fmaf(lp[j], w[2 * e + j], sl[e]);
           }
-        reinterpret_cast<float4 *>(orow + off)[q] = make_float4(sh[0], sh[1], sh[2], sh[3]);
+        {
+          typedef float native4 __attribute__((ext_vector_type(4)));
+          const native4 nv = {sh[0], sh[1], sh[2], sh[3]};
+          __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(orow + off) + q);
+        }
         reinterpret_cast<float4 *>(nxt)[q] = make_float4(sl[0], sl[1], sl[2], sl[3]);
       }
     } else {
