@@ -884,7 +884,12 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())
 #pragma unroll
   for (int b = 0; b < E / RL; b++)
 #pragma unroll
-    for (int j = 0; j < RL; j++) v[b * RL + j] = ys[reg_index<PL, RL>(t, b, j)];
+    for (int j = 0; j < RL; j++) {
+      typedef float native2 __attribute__((ext_vector_type(2)));
+      const native2 nv = __builtin_nontemporal_load(
+          reinterpret_cast<const native2 *>(ys + reg_index<PL, RL>(t, b, j)));
+      v[b * RL + j] = make_float2(nv.x, nv.y);
+    }
   fft::RegTw<PL, true> twi;
   twi.load(t, tw);
   __builtin_amdgcn_sched_barrier(0);

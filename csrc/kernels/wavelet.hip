@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256) void swt_tiled_kernel(
   const float *x = src + sig * len;
   for (int i = threadIdx.x; i < stride; i += blockDim.x) {
     const int64_t p = t0 + i;
-    in[i] = p < len ? x[p] : ext_load(x, p, len, ext);
+    in[i] = p < len ? __builtin_nontemporal_load(x + p) : ext_load(x, p, len, ext);
   }
   for (int l = 0; l < levels; l++) {
     const int dil = 1 << l;
@@ -477,7 +477,10 @@ __global__ __launch_bounds__(256) void swt_tiled_kernel(
         typedef float native4 __attribute__((ext_vector_type(4)));
         const native4 nv = {sh[0], sh[1], sh[2], sh[3]};
         __builtin_nontemporal_store(nv, reinterpret_cast<native4 *>(hrow + q));
-        if (last) reinterpret_cast<float4 *>(lo + sig * ls + t0)[q] = lv;
+        if (last) {
+          const native4 nl = {lv.x, lv.y, lv.z, lv.w};
+          __builtin_nontemporal_store(nl, reinterpret_cast<native4 *>(lo + sig * ls + t0) + q);
+        }
       }
       if (!last) reinterpret_cast<float4 *>(out)[q] = lv;
     }
@@ -651,8 +654,11 @@ __global__ __launch_bounds__(256) void dwt_multi4_kernel(
   const float *x = src + sig * len;
   float *orow = out + sig * len;
   float *bandA = dband4, *bandB = dband4 + ((len + kPad + 3) & ~3);
-  for (int q = threadIdx.x; q < len / 4; q += blockDim.x)
-    reinterpret_cast<float4 *>(bandA)[q] = reinterpret_cast<const float4 *>(x)[q];
+  for (int q = threadIdx.x; q < len / 4; q += blockDim.x) {
+    typedef float native4 __attribute__((ext_vector_type(4)));
+    const native4 nv = __builtin_nontemporal_load(reinterpret_cast<const native4 *>(x) + q);
+    reinterpret_cast<float4 *>(bandA)[q] = make_float4(nv.x, nv.y, nv.z, nv.w);
+  }
   __syncthreads();  // the level-0 extension reads samples other lanes loaded
   float *in = bandA, *nxt = bandB;
   int n = len, off = 0;
