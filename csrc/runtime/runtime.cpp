@@ -204,6 +204,13 @@ class ScratchPool {
       // graph memory node owned by the graph (freed by the matching
       // hipFreeAsync node); the cache (event queries, host-side reuse) is
       // not usable while capturing.
+      // Only small scratch is taken this way.  A captured pipeline whose
+      // scratch ran to several MiB per allocation (partitioned overlap-save
+      // spectra, tiled pyramid bands) faulted the GPU when the graph was
+      // replayed; captures of pipelines with allocations up to tens of KiB
+      // replay correctly (tests/test_graphs.py).  Larger requests are refused
+      // so such a pipeline fails at capture with an error instead.
+      if (sz > kCaptureAllocMax) return nullptr;
       void *p = nullptr;
       if (hipMallocAsync(&p, sz, stream) != hipSuccess) {
         (void)hipGetLastError();
@@ -285,6 +292,11 @@ class ScratchPool {
     return cached_;
   }
 
+  // True when alloc() refuses `bytes` because `stream` is being captured.
+  static bool refused_in_capture(size_t bytes, hipStream_t stream) {
+    return round(bytes) > kCaptureAllocMax && capturing(stream);
+  }
+
   void release_all_free() {
     std::lock_guard<std::mutex> lock(mu_);
     if (!free_.empty()) (void)hipDeviceSynchronize();
@@ -310,6 +322,7 @@ class ScratchPool {
     const size_t g = 2u << 20;
     return (b + g - 1) / g * g;
   }
+  static constexpr size_t kCaptureAllocMax = static_cast<size_t>(1) << 20;
   static bool capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (s == nullptr || hipStreamIsCapturing(s, &st) != hipSuccess) {
@@ -334,6 +347,11 @@ vs_status DeviceBuffer::alloc(size_t bytes, hipStream_t stream) {
   ptr_ = ScratchPool::get().alloc(bytes, stream);
   if (!ptr_) {
     bytes_ = 0;
+    if (ScratchPool::refused_in_capture(bytes, stream)) {
+      set_error("scratch of %zu bytes inside a stream capture is not supported (limit 1 MiB "
+                "per allocation): run this call outside the captured region", bytes);
+      return VS_ERR_UNSUPPORTED;
+    }
     set_error("device allocation of %zu bytes failed", bytes);
     return VS_ERR_ALLOC;
   }

@@ -9,6 +9,10 @@ launch.  This replaces a tracing compiler for the short, launch-bound
 pipelines the reference runs as loops of tiny calls (e.g. a filter bank over
 many small signals).
 
+Calls that need more than 1 MiB of scratch in one allocation (partitioned
+overlap-save for filters past one block, tiled pyramids of long rows, the
+four-step FFT) raise an error when captured: keep them outside the graph.
+
     g = CapturedCall(lambda x: ops.conv1d(ops.swt(x, "daubechies", 8, 3)[1], h), x0)
     y = g(x1)    # copies x1 into the static input, replays, returns the output
 """
