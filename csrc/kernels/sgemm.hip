@@ -809,15 +809,22 @@ vs_status sgemm_impl(int variant, int ta, int tb, int m, int n, int k,
       }
     }
   }
+  const auto ws_floats = [&](const Units &u) {
+    const int dim = kTileDim[tile];
+    const long tiles = static_cast<long>((m + dim - 1) / dim) * ((n + dim - 1) / dim);
+    return static_cast<size_t>(tiles - u.full) * u.slices * dim * dim * batch;
+  };
+  // inside a stream capture large scratch is not available: whole tiles only
+  if (units.slices > 1 && scratch_refused_in_capture(sizeof(float) * ws_floats(units), s)) {
+    allow_slices = false;
+    units = plan(tile);
+  }
   g.full_tiles = units.full;
   g.slices = units.slices;
   g.kchunk = units.kchunk;
   DeviceBuffer ws;
   if (units.slices > 1) {
-    const int dim = kTileDim[tile];
-    const long tiles = static_cast<long>((m + dim - 1) / dim) * ((n + dim - 1) / dim);
-    const size_t floats = static_cast<size_t>(tiles - units.full) * units.slices * dim * dim * batch;
-    VS_TRY(ws.alloc(sizeof(float) * floats, s));
+    VS_TRY(ws.alloc(sizeof(float) * ws_floats(units), s));
     g.ws = ws.as<float>();
   }
   const bool ok = launch_tile(g, ta, tb, batch, s, tile, d16);

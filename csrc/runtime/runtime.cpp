@@ -365,6 +365,9 @@ void DeviceBuffer::release() {
 }
 
 void release_cached_memory() { ScratchPool::get().release_all_free(); }
+bool scratch_refused_in_capture(size_t bytes, hipStream_t stream) {
+  return ScratchPool::refused_in_capture(bytes, stream);
+}
 
 // ------------------------------------------------------- packed staging
 namespace {

@@ -126,6 +126,10 @@ class DeviceBuffer {
 
 // Frees every cached (unused) pool block.
 void release_cached_memory();
+// True when a DeviceBuffer of `bytes` would be refused because `stream` is
+// being captured into a graph (scratch above 1 MiB per allocation is not
+// taken inside a capture): callers with a scratch-free alternative use it.
+bool scratch_refused_in_capture(size_t bytes, hipStream_t stream);
 
 // ----------------------------------------------------------- staging
 // Staging context of one host-API call (api::run_sync opens one per call).

@@ -89,6 +89,24 @@ def test_capture_refuses_large_scratch():
     torch.testing.assert_close(ops.conv1d(x, h, algorithm="overlap_save"), want)
 
 
+@pytest.mark.gpu
+def test_capture_sgemm_with_sliced_tail_uses_whole_tiles():
+    """3072^3 runs with its tail tiles cut into k slices (a workspace of
+    several MiB) when called eagerly; inside a capture the planner falls
+    back to whole tiles (no scratch) and the replays match."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = torch.randn(3072, 3072, device="cuda", generator=g)
+    b = torch.randn(3072, 3072, device="cuda", generator=g)
+    cap = CapturedCall(ops.sgemm, a, b)
+    for seed in (1, 2, 3):
+        g2 = torch.Generator(device="cuda").manual_seed(seed)
+        a2 = torch.randn(a.shape, device="cuda", generator=g2)
+        b2 = torch.randn(b.shape, device="cuda", generator=g2)
+        got = cap(a2, b2).clone()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(got, ops.sgemm(a2, b2), rtol=1e-4, atol=1e-2)
+
+
 def test_capture_requires_gpu():
     if torch.cuda.is_available():
         pytest.skip("GPU present")
