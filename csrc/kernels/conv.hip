@@ -1438,7 +1438,9 @@ int vs_conv1d_os_block(int hlen) { return 1 << conv::os_block_log(hlen); }
 }  // extern "C"
 
 struct vs_conv_plan {
-  int algo, correlate, xlen, hlen, nfilt;
+  int algo, correlate;
+  int64_t xlen;
+  int hlen, nfilt;
   bool overlap_save;  // real plans: overlap-save blocks vs one block
   int logl;           // real plans: block of 2^logl samples
   int parts;          // > 0: partitioned overlap-save, filter partitions
@@ -1448,17 +1450,19 @@ struct vs_conv_plan {
 
 extern "C" {
 
-vs_status vs_conv1d_plan_create(int algo, int correlate, int xlen, const float *h, int hlen,
+vs_status vs_conv1d_plan_create(int algo, int correlate, int64_t xlen, const float *h, int hlen,
                                 int64_t hs, int nfilt, vs_conv_plan **plan,
                                 vs_stream_t stream) {
   VS_REQUIRE(plan && h, "vs_conv1d_plan_create: null pointer");
   *plan = nullptr;
   VS_REQUIRE(xlen > 0 && hlen > 0 && nfilt >= 1, "vs_conv1d_plan_create: empty shape");
   VS_REQUIRE(nfilt == 1 || hs >= hlen, "vs_conv1d_plan_create: filter stride < filter length");
+  VS_REQUIRE(hlen < (1 << 30), "vs_conv1d_plan_create: filter of %d taps too long", hlen);
   const long long ylen = static_cast<long long>(xlen) + hlen - 1;
-  VS_REQUIRE(ylen < (1LL << 31), "vs_conv1d_plan_create: output too long");
   auto s = static_cast<hipStream_t>(stream);
   if (algo == VS_CONV_AUTO) algo = conv::select(xlen, hlen, nfilt);
+  // rows cut into pieces (vs_conv1d_plan_execute) run overlap-save blocks
+  if (ylen > conv::max_call_out() && algo == VS_CONV_FFT) algo = VS_CONV_OVERLAP_SAVE;
   VS_REQUIRE(algo >= VS_CONV_DIRECT && algo <= VS_CONV_OVERLAP_SAVE,
              "vs_conv1d_plan_create: unknown algorithm %d", algo);
   // The real-block path vs_conv1d would take for this shape, if any
@@ -1535,7 +1539,7 @@ vs_status vs_conv1d_plan_execute(const vs_conv_plan *p, const float *x, int64_t 
              "vs_conv1d_plan_execute: plan has %d per-signal filters, batch %d", p->nfilt,
              batch);
   if (batch == 0) return VS_OK;
-  const int ylen = p->xlen + p->hlen - 1;
+  const long long ylen = static_cast<long long>(p->xlen) + p->hlen - 1;
   VS_REQUIRE(batch <= 1 || (xs >= p->xlen && ys >= ylen),
              "vs_conv1d_plan_execute: row strides smaller than the rows");
   auto s = static_cast<hipStream_t>(stream);
@@ -1548,14 +1552,28 @@ vs_status vs_conv1d_plan_execute(const vs_conv_plan *p, const float *x, int64_t 
       return vs_conv1d_plan_execute(p, x + b0 * xs, xs, y + b0 * ys, ys, nb, stream);
     });
   }
-  // h is not read when the spectra are precomputed; hs only flags per-signal P / Q
-  if (p->parts)
-    return conv::run_partitioned(p->correlate, x, p->xlen, xs, nullptr, p->hlen,
-                                 p->nfilt > 1 ? p->hlen : 0, y, ys, ylen, batch, s, p->pq,
-                                 p->logl);
-  return conv::run_real(p->correlate, p->overlap_save, x, p->xlen, xs, nullptr, p->hlen,
-                        p->nfilt > 1 ? p->hlen : 0, y, ys, ylen, ylen, 0, batch, s, p->pq,
-                        p->logl);
+  // h is not read when the spectra are precomputed; hs only flags per-signal P / Q.
+  // One launch sequence over x[x0, x0 + xl) writing its first `outs` outputs at yy.
+  const int64_t hs = p->nfilt > 1 ? p->hlen : 0;
+  const auto run = [&](const float *xx, int xl, float *yy, int outs) {
+    if (p->parts)
+      return conv::run_partitioned(p->correlate, xx, xl, xs, nullptr, p->hlen, hs, yy, ys, outs,
+                                   batch, s, p->pq, p->logl);
+    return conv::run_real(p->correlate, p->overlap_save, xx, xl, xs, nullptr, p->hlen, hs, yy, ys,
+                          outs, outs, 0, batch, s, p->pq, p->logl);
+  };
+  if (ylen <= conv::max_call_out())
+    return run(x, static_cast<int>(p->xlen), y, static_cast<int>(ylen));
+  // long rows: the pieces of vs_conv1d, last to first, with the plan's spectra
+  const long long piece = conv::piece_out();
+  for (long long c = (ylen + piece - 1) / piece - 1; c >= 0; c--) {
+    const long long o0 = c * piece;
+    const long long olen = std::min(piece, ylen - o0);
+    const long long x0 = std::max<long long>(0, o0 - (p->hlen - 1));
+    const long long x1 = std::min<long long>(p->xlen, o0 + olen);
+    VS_TRY(run(x + x0, static_cast<int>(x1 - x0), y + x0, static_cast<int>(o0 - x0 + olen)));
+  }
+  return VS_OK;
 }
 
 vs_status vs_conv1d_plan_info(const vs_conv_plan *p, int *algo, int *precomputed) {

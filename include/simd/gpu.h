@@ -265,7 +265,7 @@ int vs_conv1d_os_block(int h_len);
 /// pointer; copied / transformed during creation, on `stream`).
 /// n_filters = 1 (shared filter, any batch) or the batch (one per signal).
 typedef struct vs_conv_plan vs_conv_plan;
-vs_status vs_conv1d_plan_create(int algo, int correlate, int x_len, const float *h,
+vs_status vs_conv1d_plan_create(int algo, int correlate, int64_t x_len, const float *h,
                                 int h_len, int64_t h_stride, int n_filters,
                                 vs_conv_plan **plan, vs_stream_t stream);
 /// y[b] = x[b] (*) h of the plan; the same contract as vs_conv1d.

@@ -364,3 +364,46 @@ def test_direct_small_vector_and_scalar_paths(hlen, xlen, off, correlate, packed
     got = yb[off:off + batch * ys].reshape(batch, ys)
     assert (got[:, :ylen].double() - want).abs().max().item() < 1e-4
     assert (got[:, ylen:] == 3.0).all()
+
+
+@pytest.mark.slow
+def test_fft_batch_beyond_2p31_elements():
+    """Batched c2c FFT whose arrays hold 2^32 + 48 complex numbers
+    (2^28 + 3 transforms of 16 points): 64-bit offsets across the batch
+    chunks; spot rows against torch.fft."""
+    import torch
+    from veles.simd_amd import ops
+    n, batch = 16, (1 << 28) + 3
+    z = torch.empty(batch, n, 2, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(8)
+    step = 1 << 24
+    for a in range(0, batch, step):
+        z[a:a + step].normal_(generator=g)
+    f = ops.fft(z)
+    rows = torch.tensor([0, 1, 65534, 65535, 65536, (1 << 27) - 1, 1 << 27, (1 << 28) - 1, 1 << 28,
+                         batch - 1], device="cuda")
+    want = torch.view_as_real(torch.fft.fft(torch.view_as_complex(z[rows].double()), dim=-1))
+    assert (f[rows].double() - want).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("hlen,per_signal", [(1000, False), (4096, True), (40000, False)])
+@pytest.mark.parametrize("corr", [False, True])
+def test_plan_rows_cut_into_pieces(hlen, per_signal, corr):
+    """vs_conv1d_plan_execute on rows longer than one launch sequence: the
+    pieces of vs_conv1d with the plan's precomputed spectra (single-block
+    overlap-save and partitioned plans, shared and per-signal filters)."""
+    import torch
+    from veles.simd_amd import ops
+    batch, xlen = 2, 100003
+    g = torch.Generator().manual_seed(hlen)
+    x = torch.randn(batch, xlen, generator=g)
+    h = torch.randn(batch if per_signal else 1, hlen, generator=g)
+    hd = h.cuda() if per_signal else h[0].cuda()
+    with _knob("conv_piece_log", 14, 28):
+        plan = ops.Conv1dPlan(hd, xlen, algorithm="overlap_save", correlate=corr)
+        assert plan.precomputed
+        y = plan(x.cuda()).cpu().double().numpy()
+    for b in range(batch):
+        ref = _fft_ref(x[b].numpy(), h[b if per_signal else 0].numpy(), corr)
+        tol = 2e-6 * np.sqrt(hlen) * np.abs(x[b].numpy()).max() * np.abs(h.numpy()).max() * 30
+        assert np.abs(y[b] - ref).max() <= tol + 1e-4

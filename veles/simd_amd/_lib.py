@@ -87,7 +87,7 @@ _SIGNATURES = {
     "vs_conv1d": (_i, [_i, _i, _vp, _i64, _i64, _vp, _i, _i64, _vp, _i64, _i,
                        _vp]),
     "vs_conv1d_select": (_i, [_i64, _i, _i]),
-    "vs_conv1d_plan_create": (_i, [_i, _i, _i, _vp, _i, _i64, _i, ctypes.POINTER(_vp), _vp]),
+    "vs_conv1d_plan_create": (_i, [_i, _i, _i64, _vp, _i, _i64, _i, ctypes.POINTER(_vp), _vp]),
     "vs_conv1d_plan_execute": (_i, [_vp, _vp, _i64, _vp, _i64, _i, _vp]),
     "vs_conv1d_plan_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "vs_conv1d_plan_destroy": (None, [_vp]),
