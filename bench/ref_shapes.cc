@@ -176,8 +176,13 @@ void floor_rows() {
          wait();
        }));
   std::vector<float> a(4, 1.f), b(4, 2.f), c(4);
-  emit("floor_host_api_matrix_add_2x2",
+  // a 2 x 2 call stays on the host (small-call policy); 128 x 128 is the
+  // smallest add that makes the GPU round trip
+  emit("host_api_matrix_add_2x2",
        time_us(20000, [&] { matrix_add(1, a.data(), b.data(), 2, 2, c.data()); }));
+  std::vector<float> a2(16384, 1.f), b2(16384, 2.f), c2(16384);
+  emit("floor_host_api_matrix_add_128x128",
+       time_us(20000, [&] { matrix_add(1, a2.data(), b2.data(), 128, 128, c2.data()); }));
   {  // the PCIe share of the 300x256 . 256x1000 host call: A and B in, C out
     const size_t in_b = (300 * 256 + 256 * 1000) * sizeof(float), out_b = 300 * 1000 * sizeof(float);
     void *hin = vs_host_alloc(in_b), *hout = vs_host_alloc(out_b), *din = nullptr, *dout = nullptr;

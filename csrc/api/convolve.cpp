@@ -62,10 +62,27 @@ void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl
   });
 }
 
+// Convolutions (direct calls and handles alike) below this many multiply-adds run the vectorised host
+// loops even with simd = 1 when every operand is in host memory: a GPU round
+// trip (stage in, launch, stage out, sync) costs 16-18 us on MI355X, the
+// host loop 0.02-0.05 ns per MAC (profiles/r3/hostapi).  VELES_HOST_MAX_MACS.
+size_t host_max_macs() {
+  static const size_t v = [] {
+    const char *e = std::getenv("VELES_HOST_MAX_MACS");
+    return e && *e ? static_cast<size_t>(std::atoll(e)) : static_cast<size_t>(1) << 19;
+  }();
+  return v;
+}
+
 void run_plan(const char *what, ConvPlan *plan, int reverse, const float *x,
               const float *h, float *result) {
   if (!plan || !x || !h || !result) vs::fatal("%s: invalid arguments", what);
-  if (vs::gpu_available()) {
+  const bool tiny = plan->x_length * plan->h_length < host_max_macs() &&
+                    !vs::api::any_device({x, h, result});
+  if (tiny) {  // the direct sum on the host beats a transform and a GPU round trip
+    if (reverse) vs::host::correlate_direct(x, plan->x_length, h, plan->h_length, result);
+    else vs::host::convolve_direct(x, plan->x_length, h, plan->h_length, result);
+  } else if (vs::gpu_available()) {
     gpu_conv(what, plan->algorithm, reverse, x, plan->x_length, h, plan->h_length,
              result);
   } else {
@@ -164,28 +181,19 @@ ConvolutionHandle auto_init(size_t xl, size_t hl, int reverse) {
   return h;
 }
 
-// Direct convolutions below this many multiply-adds run the host reference
-// even with simd = 1 when every operand is in host memory: a GPU round trip
-// (stage in, launch, stage out, sync) costs ~40 us on MI355X, the host loop
-// ~0.3 ns per MAC (profiles/r1/reference_shapes.json).  VELES_HOST_MAX_MACS.
-size_t host_max_macs() {
-  static const size_t v = [] {
-    const char *e = std::getenv("VELES_HOST_MAX_MACS");
-    return e && *e ? static_cast<size_t>(std::atoll(e)) : static_cast<size_t>(1) << 17;
-  }();
-  return v;
-}
-
 void direct(const char *what, int simd, int reverse, const float *x, size_t xl,
             const float *h, size_t hl, float *result) {
   if (!x || !h || !result || !xl || !hl) vs::fatal("%s: invalid arguments", what);
   const bool tiny = xl * hl < host_max_macs() && !vs::api::any_device({x, h, result});
   if (!tiny && vs::api::use_gpu_simd(simd, what)) {
     gpu_conv(what, VS_CONV_DIRECT, reverse, x, xl, h, hl, result);
-  } else if (reverse) {
-    vs::ref::correlate_direct(x, xl, h, hl, result);
+  } else if (simd == 0) {  // the scalar reference
+    if (reverse) vs::ref::correlate_direct(x, xl, h, hl, result);
+    else vs::ref::convolve_direct(x, xl, h, hl, result);
+  } else if (reverse) {    // tiny or no GPU: vectorised host loops
+    vs::host::correlate_direct(x, xl, h, hl, result);
   } else {
-    vs::ref::convolve_direct(x, xl, h, hl, result);
+    vs::host::convolve_direct(x, xl, h, hl, result);
   }
 }
 

@@ -45,6 +45,13 @@ inline bool use_gpu_simd(int simd, const char *fn) {
   return false;
 }
 
+// simd != 0 calls on host operands whose work is below `limit` (elements or
+// multiply-adds, scaled by VELES_HOST_SMALL_SCALE percent) run vectorised host
+// loops: the GPU round trip alone costs 14-18 us.
+inline bool host_small(size_t work, size_t limit, std::initializer_list<const void *> ptrs) {
+  return work < limit * host_small_scale() / 100 && !any_device(ptrs);
+}
+
 inline bool use_gpu_array(size_t n, std::initializer_list<const void *> ptrs) {
   if (!gpu_available()) return false;
   return n >= gpu_min_elems() || any_device(ptrs);

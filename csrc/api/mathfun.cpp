@@ -10,9 +10,14 @@
 #include "simd/gpu.h"
 
 namespace {
+// Arrays this short run libm on the host even with simd = 1 (about 10 ns per
+// element against a GPU round trip of 14-18 us).
+constexpr size_t kSmallElems = 1024;
+
 void psv(int simd, int fn, const char *what, PsvStdFunc host, const float *src,
          size_t n, float *res) {
-  if (!vs::api::use_gpu_simd(simd, what) || n == 0) {
+  if (!vs::api::use_gpu_simd(simd, what) || n == 0 ||
+      vs::api::host_small(n, kSmallElems, {src, res})) {
     func_psv_novec(host, src, n, res);
     return;
   }
@@ -45,7 +50,8 @@ void sqrt_psv(int simd, const float *src, size_t n, float *res) {
 }
 
 void sincos_psv(int simd, const float *src, size_t n, float *s, float *c) {
-  if (!vs::api::use_gpu_simd(simd, "sincos_psv") || n == 0) {
+  if (!vs::api::use_gpu_simd(simd, "sincos_psv") || n == 0 ||
+      vs::api::host_small(n, kSmallElems, {src, s, c})) {
     sincos_psv_novec(src, n, s, c);
     return;
   }
@@ -63,7 +69,8 @@ void sincos_psv(int simd, const float *src, size_t n, float *s, float *c) {
 }
 
 void pow_psv(int simd, const float *x, const float *y, size_t n, float *res) {
-  if (!vs::api::use_gpu_simd(simd, "pow_psv") || n == 0) {
+  if (!vs::api::use_gpu_simd(simd, "pow_psv") || n == 0 ||
+      vs::api::host_small(n, kSmallElems / 2, {x, y, res})) {
     pow_psv_novec(x, y, n, res);
     return;
   }

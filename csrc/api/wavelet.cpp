@@ -82,7 +82,7 @@ void wavelet_apply(WaveletType type, int order, ExtensionType ext,
   // Flag-less API (like arithmetic.h): GPU for device operands or enough
   // work (length x taps) to amortise the host<->device round trip.
   if (!vs::api::use_gpu_array(length * order, {src, desthi, destlo})) {
-    vs::ref::dwt(type, order, ext, src, length, desthi, destlo);
+    vs::host::dwt(type, order, ext, src, length, desthi, destlo);
     return;
   }
   vs::api::run_sync("wavelet_apply", [&](hipStream_t s) {
@@ -115,7 +115,7 @@ void stationary_wavelet_apply(WaveletType type, int order, int level,
                  desthi, destlo);
   if (level < 1) vs::fatal("stationary_wavelet_apply: level %d < 1", level);
   if (!vs::api::use_gpu_array(length * order, {src, desthi, destlo})) {
-    vs::ref::swt(type, order, level, ext, src, length, desthi, destlo);
+    vs::host::swt(type, order, level, ext, src, length, desthi, destlo);
     return;
   }
   vs::api::run_sync("stationary_wavelet_apply", [&](hipStream_t s) {

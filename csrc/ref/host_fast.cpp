@@ -1,0 +1,298 @@
+// Host paths for calls too small to be worth a GPU round trip (about 11 us of
+// launch + wait on MI355X): direct convolution / correlation and single
+// wavelet levels on a few hundred samples.  The scalar functions of ref.cpp
+// stay the semantic reference (simd = 0, `_na`); these compute the same sums
+// with unit-stride inner loops the host compiler vectorises, built for the
+// baseline ISA and for AVX2 + FMA with load-time dispatch (target_clones).
+// The reference's counterparts are its hand-written AVX loops
+// (reference src/convolve.c:49-100, src/wavelet.c:395-1555).
+// Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "csrc/data/wavelet_tables.h"
+#include "csrc/ref/ref.h"
+
+// Every loop body below is an always-inline function instantiated twice: for
+// the baseline ISA and inside a function compiled for AVX2 + FMA, chosen once
+// per process by CPU feature (`arch=` clones would match one CPU model only).
+// (hipcc also parses this file for the device, where neither applies.)
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#define VS_HOST_AVX2 1
+#define VS_TARGET_AVX2 __attribute__((target("avx2,fma")))
+#else
+#define VS_HOST_AVX2 0
+#define VS_TARGET_AVX2
+#endif
+#define VS_BODY static inline __attribute__((always_inline))
+
+// multiply-adds of this file may fuse (the rest of the host code is built
+// with contraction off to match the scalar reference bit for bit)
+#pragma clang fp contract(fast)
+
+namespace vs {
+namespace host {
+namespace {
+
+// y[0 .. n) += a * x[0 .. n)
+VS_BODY void axpy_body(float a, const float *__restrict__ x, float *__restrict__ y, long n) {
+  for (long i = 0; i < n; i++) y[i] += a * x[i];
+}
+
+// y[n] = sum_m h[m] xp[n - m] for n in [0, ny), 64 outputs at a time held in
+// registers over the whole tap loop: one load + one FMA per 8 products.
+// xp points at x[0] inside a copy of x with 63 zeros before it and 63 after
+// it (only taps that reach a real sample of the block are visited).
+constexpr long kConvBlock = 64;
+typedef float V8 __attribute__((vector_size(32)));
+typedef float V8u __attribute__((vector_size(32), aligned(4)));
+VS_BODY void conv_blocked_body(const float *__restrict__ xp, const float *__restrict__ h,
+                              long nh, float *__restrict__ y, long ny) {
+  const long nx = ny - nh + 1;
+  for (long n0 = 0; n0 < ny; n0 += kConvBlock) {
+    V8 a0 = {}, a1 = {}, a2 = {}, a3 = {}, a4 = {}, a5 = {}, a6 = {}, a7 = {};
+    const float *p = xp + n0;
+    // taps whose 64 samples are not all padding: n - m in [0, nx)
+    const long m0 = std::max(0L, n0 - (nx - 1)), m1 = std::min(nh, n0 + kConvBlock);
+    for (long m = m0; m < m1; m++) {
+      const float hs = h[m];
+      const V8 hm = {hs, hs, hs, hs, hs, hs, hs, hs};
+      const V8u *q = reinterpret_cast<const V8u *>(p - m);
+      a0 += hm * q[0];
+      a1 += hm * q[1];
+      a2 += hm * q[2];
+      a3 += hm * q[3];
+      a4 += hm * q[4];
+      a5 += hm * q[5];
+      a6 += hm * q[6];
+      a7 += hm * q[7];
+    }
+    float acc[kConvBlock];
+    V8u *o = reinterpret_cast<V8u *>(acc);
+    o[0] = a0, o[1] = a1, o[2] = a2, o[3] = a3, o[4] = a4, o[5] = a5, o[6] = a6, o[7] = a7;
+    const long w = std::min(kConvBlock, ny - n0);
+    for (long j = 0; j < w; j++) y[n0 + j] = acc[j];
+  }
+}
+
+// Two-channel filter bank over unit-stride runs: out[d] = sum_j c[j] run_j[d].
+// The decimated level reads even / odd samples (tap j at offset j / 2 of ev
+// or od), the stationary level one array (od = nullptr, tap j at offset
+// j * stride).  16 outputs of both bands stay
+// in registers over the tap loop.  The runs must be readable 15 floats past
+// the last output.
+VS_BODY void bank_body(const float *__restrict__ hp, const float *__restrict__ lp, int order,
+                       const float *__restrict__ ev, const float *__restrict__ od,
+                       long stride, float *__restrict__ hi, float *__restrict__ lo, long n) {
+  for (long d0 = 0; d0 < n; d0 += 16) {
+    V8 h0 = {}, h1 = {}, l0 = {}, l1 = {};
+    for (int j = 0; j < order; j++) {
+      const float *run = od ? ((j & 1) ? od : ev) + (j >> 1) + d0 : ev + j * stride + d0;
+      const V8u *q = reinterpret_cast<const V8u *>(run);
+      const float a = hp[j], b = lp[j];
+      const V8 va = {a, a, a, a, a, a, a, a}, vb = {b, b, b, b, b, b, b, b};
+      const V8 x0 = q[0], x1 = q[1];
+      h0 += va * x0;
+      h1 += va * x1;
+      l0 += vb * x0;
+      l1 += vb * x1;
+    }
+    if (d0 + 16 <= n) {
+      V8u *oh = reinterpret_cast<V8u *>(hi + d0), *ol = reinterpret_cast<V8u *>(lo + d0);
+      oh[0] = h0, oh[1] = h1, ol[0] = l0, ol[1] = l1;
+    } else {
+      float th[16], tl[16];
+      V8u *oh = reinterpret_cast<V8u *>(th), *ol = reinterpret_cast<V8u *>(tl);
+      oh[0] = h0, oh[1] = h1, ol[0] = l0, ol[1] = l1;
+      for (long j = 0; d0 + j < n; j++) hi[d0 + j] = th[j], lo[d0 + j] = tl[j];
+    }
+  }
+}
+
+// Even and odd samples of src[0 .. 2 half) into ev / od.
+VS_BODY void split_body(const float *__restrict__ src, long half, float *__restrict__ ev,
+                        float *__restrict__ od) {
+  for (long d = 0; d < half; d++) {
+    ev[d] = src[2 * d];
+    od[d] = src[2 * d + 1];
+  }
+}
+
+// out[i] = a[i] + sign * b[i]
+VS_BODY void addsub_body(const float *__restrict__ a, const float *__restrict__ b, float sign,
+                         float *__restrict__ out, long n) {
+  for (long i = 0; i < n; i++) out[i] = a[i] + sign * b[i];
+}
+
+// dot product with eight-lane partial sums
+VS_BODY void dot_body(const float *__restrict__ a, const float *__restrict__ b, long n,
+                      float *__restrict__ out) {
+  V8 acc = {};
+  long i = 0;
+  for (; i + 8 <= n; i += 8)
+    acc += *reinterpret_cast<const V8u *>(a + i) * *reinterpret_cast<const V8u *>(b + i);
+  float r = ((acc[0] + acc[4]) + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7]));
+  for (; i < n; i++) r += a[i] * b[i];
+  *out = r;
+}
+
+bool have_avx2() {
+#if VS_HOST_AVX2
+  static const bool yes = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+  return yes;
+#else
+  return false;
+#endif
+}
+
+#define VS_DISPATCH(name, params, args)                              \
+  VS_TARGET_AVX2 void name##_avx2 params { name##_body args; }       \
+  void name##_base params { name##_body args; }                      \
+  inline void name params {                                          \
+    if (have_avx2()) name##_avx2 args;                               \
+    else name##_base args;                                           \
+  }
+VS_DISPATCH(axpy, (float a, const float *x, float *y, long n), (a, x, y, n))
+VS_DISPATCH(conv_blocked, (const float *xp, const float *h, long nh, float *y, long ny),
+            (xp, h, nh, y, ny))
+VS_DISPATCH(bank, (const float *hp, const float *lp, int order, const float *ev,
+                   const float *od, long stride, float *hi, float *lo, long n),
+            (hp, lp, order, ev, od, stride, hi, lo, n))
+VS_DISPATCH(split, (const float *src, long half, float *ev, float *od), (src, half, ev, od))
+VS_DISPATCH(addsub, (const float *a, const float *b, float sign, float *out, long n),
+            (a, b, sign, out, n))
+VS_DISPATCH(dot, (const float *a, const float *b, long n, float *out), (a, b, n, out))
+#undef VS_DISPATCH
+
+float extended(const float *src, long len, long idx, ExtensionType ext) {
+  if (idx < len) return src[idx];
+  const long t = idx - len;
+  switch (ext) {
+    case EXTENSION_TYPE_PERIODIC: return src[t % len];
+    case EXTENSION_TYPE_MIRROR: return src[len - 1 - (t % len)];
+    case EXTENSION_TYPE_CONSTANT: return src[len - 1];
+    default: return 0.f;
+  }
+}
+
+std::vector<float> &scratch(int which) {
+  static thread_local std::vector<float> buf[2];
+  return buf[which];
+}
+
+// Many taps: the axpy form moves three vectors per FMA; keep the outputs in
+// registers instead.  The shorter operand plays the filter.
+constexpr long kBlockedMinTaps = 24;
+void blocked(const float *x, long nx, const float *h, long nh, bool reverse_h, float *y) {
+  std::vector<float> &hr = scratch(1);
+  if (reverse_h) {
+    hr.resize(static_cast<size_t>(nh));
+    std::reverse_copy(h, h + nh, hr.begin());
+    h = hr.data();
+  }
+  if (nx < nh) {
+    std::swap(x, h);
+    std::swap(nx, nh);
+  }
+  std::vector<float> &xp = scratch(0);
+  const long ny = nx + nh - 1;
+  xp.resize(static_cast<size_t>(nx + 2 * kConvBlock));
+  std::fill_n(xp.begin(), kConvBlock, 0.f);
+  std::memcpy(xp.data() + kConvBlock, x, sizeof(float) * static_cast<size_t>(nx));
+  std::fill_n(xp.begin() + kConvBlock + nx, kConvBlock, 0.f);
+  conv_blocked(xp.data() + kConvBlock, h, nh, y, ny);
+}
+
+}  // namespace
+
+// y[n] = sum_m h[m] x[n - m]: one pass of y[m ..] += h[m] * x per tap, taps
+// in increasing order (the order ref::convolve_direct adds them in).
+void convolve_direct(const float *x, size_t xl, const float *h, size_t hl, float *y) {
+  const long nx = static_cast<long>(xl), nh = static_cast<long>(hl);
+  if (std::min(nx, nh) >= kBlockedMinTaps) return blocked(x, nx, h, nh, false, y);
+  std::memset(y, 0, sizeof(float) * static_cast<size_t>(nx + nh - 1));
+  if (nx >= nh) {
+    for (long m = 0; m < nh; m++) axpy(h[m], x, y + m, nx);
+  } else {  // the longer operand in the inner loop
+    for (long m = 0; m < nx; m++) axpy(x[m], h, y + m, nh);
+  }
+}
+
+// r[k] = sum_m x[m] h[m + H - 1 - k]: the convolution with the reversed filter.
+void correlate_direct(const float *x, size_t xl, const float *h, size_t hl, float *y) {
+  const long nx = static_cast<long>(xl), nh = static_cast<long>(hl);
+  if (std::min(nx, nh) >= kBlockedMinTaps) return blocked(x, nx, h, nh, true, y);
+  std::memset(y, 0, sizeof(float) * static_cast<size_t>(nx + nh - 1));
+  if (nx >= nh) {
+    for (long m = 0; m < nh; m++) axpy(h[nh - 1 - m], x, y + m, nx);
+  } else {
+    std::vector<float> &hr = scratch(0);
+    hr.resize(hl);
+    std::reverse_copy(h, h + nh, hr.begin());
+    for (long m = 0; m < nx; m++) axpy(x[m], hr.data(), y + m, nh);
+  }
+}
+
+// One decimated level: the extended signal split into its even and odd
+// samples, so tap j reads a unit-stride run of one of them.
+void dwt(WaveletType type, int order, ExtensionType ext, const float *src, size_t len,
+         float *hi, float *lo) {
+  float hp[wavelet_tables::kMaxOrder], lp[wavelet_tables::kMaxOrder];
+  wavelet_tables::make_filters(wavelet_tables::lowpass_f(type, order), order, hp, lp);
+  const long n = static_cast<long>(len), half = n / 2;
+  const long m = half + (order + 1) / 2;  // even / odd samples a level touches
+  std::vector<float> &ev = scratch(0), &od = scratch(1);
+  ev.resize(static_cast<size_t>(m + 16));
+  od.resize(static_cast<size_t>(m + 16));
+  split(src, half, ev.data(), od.data());
+  for (long d = half; d < m; d++) {
+    ev[d] = extended(src, n, 2 * d, ext);
+    od[d] = extended(src, n, 2 * d + 1, ext);
+  }
+  bank(hp, lp, order, ev.data(), od.data(), 0, hi, lo, half);  // x~[2 d + j]
+}
+
+// One stationary level: tap r reads the extended signal at offset r 2^(level-1).
+void swt(WaveletType type, int order, int level, ExtensionType ext, const float *src,
+         size_t len, float *hi, float *lo) {
+  float hp[wavelet_tables::kMaxOrder], lp[wavelet_tables::kMaxOrder];
+  wavelet_tables::make_filters(wavelet_tables::lowpass_f(type, order), order, hp, lp);
+  const long stride = 1L << (level - 1);
+  const long n = static_cast<long>(len);
+  const long m = n + (order - 1) * stride;
+  std::vector<float> &xe = scratch(0);
+  xe.resize(static_cast<size_t>(m + 16));
+  std::memcpy(xe.data(), src, sizeof(float) * len);
+  for (long i = n; i < m; i++) xe[i] = extended(src, n, i, ext);
+  bank(hp, lp, order, xe.data(), nullptr, stride, hi, lo, n);
+}
+
+void matrix_add(const float *a, const float *b, size_t w, size_t h, float *res) {
+  addsub(a, b, 1.f, res, static_cast<long>(w * h));
+}
+
+void matrix_sub(const float *a, const float *b, size_t w, size_t h, float *res) {
+  addsub(a, b, -1.f, res, static_cast<long>(w * h));
+}
+
+// res (h1 x w2) = a (h1 x w1) b (w1 x w2): row i of res accumulates
+// a[i][k] * (row k of b), unit stride over w2.
+void matrix_multiply(const float *a, const float *b, size_t w1, size_t h1, size_t w2,
+                     float *res) {
+  std::memset(res, 0, sizeof(float) * h1 * w2);
+  for (size_t i = 0; i < h1; i++)
+    for (size_t k = 0; k < w1; k++)
+      axpy(a[i * w1 + k], b + k * w2, res + i * w2, static_cast<long>(w2));
+}
+
+// res (h1 x h2) = a (h1 x w1) b^T, b stored h2 x w1: row-by-row dot products.
+void matrix_multiply_transposed(const float *a, const float *b, size_t w1, size_t h1,
+                                size_t h2, float *res) {
+  for (size_t i = 0; i < h1; i++)
+    for (size_t j = 0; j < h2; j++)
+      dot(a + i * w1, b + j * w1, static_cast<long>(w1), res + i * h2 + j);
+}
+
+}  // namespace host
+}  // namespace vs

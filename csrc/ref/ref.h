@@ -58,4 +58,21 @@ void swt(WaveletType type, int order, int level, ExtensionType ext,
          const float *src, size_t len, float *hi, float *lo);
 
 }  // namespace ref
+
+// Vectorised host paths for tiny calls (csrc/ref/host_fast.cpp): the same
+// sums as the scalar reference above, unit-stride inner loops.
+namespace host {
+void convolve_direct(const float *x, size_t xl, const float *h, size_t hl, float *y);
+void correlate_direct(const float *x, size_t xl, const float *h, size_t hl, float *y);
+void dwt(WaveletType type, int order, ExtensionType ext, const float *src, size_t len,
+         float *hi, float *lo);
+void swt(WaveletType type, int order, int level, ExtensionType ext, const float *src,
+         size_t len, float *hi, float *lo);
+void matrix_add(const float *a, const float *b, size_t w, size_t h, float *res);
+void matrix_sub(const float *a, const float *b, size_t w, size_t h, float *res);
+void matrix_multiply(const float *a, const float *b, size_t w1, size_t h1, size_t w2,
+                     float *res);
+void matrix_multiply_transposed(const float *a, const float *b, size_t w1, size_t h1,
+                                size_t h2, float *res);
+}  // namespace host
 }  // namespace vs

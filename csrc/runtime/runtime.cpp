@@ -1,7 +1,10 @@
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include "csrc/runtime/runtime.h"
 
+#include <unistd.h>
+
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
@@ -101,8 +104,34 @@ hipStream_t library_stream() {
   return streams[dev];
 }
 
+// The program break heap [start_brk, sbrk(0)) belongs to malloc: no device or
+// pinned allocation can live there, so small malloc'd operands (the tiny host
+// calls, where three hipPointerGetAttributes queries of ~0.1 us each would
+// cost more than the work) are classified without asking the HIP runtime.
+static bool in_brk_heap(const void *p) {
+  static const uintptr_t start = [] {
+    // field 47 of /proc/self/stat (after the parenthesised command name)
+    uintptr_t v = 0;
+    if (FILE *f = std::fopen("/proc/self/stat", "r")) {
+      char buf[2048];
+      const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+      std::fclose(f);
+      buf[n] = 0;
+      if (const char *q = std::strrchr(buf, ')')) {
+        int field = 2;
+        for (q++; *q && field < 47; q++)
+          if (*q == ' ') field++;
+        if (field == 47) v = static_cast<uintptr_t>(std::strtoull(q, nullptr, 10));
+      }
+    }
+    return v;
+  }();
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return start && a >= start && a < reinterpret_cast<uintptr_t>(sbrk(0));
+}
+
 bool is_device_pointer(const void *p) {
-  if (!p || !gpu_available()) return false;
+  if (!p || !gpu_available() || in_brk_heap(p)) return false;
   hipPointerAttribute_t attr;
   if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
     (void)hipGetLastError();
@@ -116,6 +145,15 @@ size_t gpu_min_elems() {
   static const size_t n = [] {
     const char *v = std::getenv("VELES_GPU_MIN_ELEMS");
     if (!v || !*v) return static_cast<size_t>(1) << 20;
+    return static_cast<size_t>(std::strtoull(v, nullptr, 10));
+  }();
+  return n;
+}
+
+size_t host_small_scale() {
+  static const size_t n = [] {
+    const char *v = std::getenv("VELES_HOST_SMALL_SCALE");
+    if (!v || !*v) return static_cast<size_t>(100);
     return static_cast<size_t>(std::strtoull(v, nullptr, 10));
   }();
   return n;
@@ -512,7 +550,7 @@ vs_status wait_stream(hipStream_t s) {
 enum class MemKind { kDevice, kPinned, kPageable };
 static MemKind classify(const void *p, void **mapped) {
   *mapped = nullptr;
-  if (!p || !gpu_available()) return MemKind::kPageable;
+  if (!p || !gpu_available() || in_brk_heap(p)) return MemKind::kPageable;
   hipPointerAttribute_t attr;
   if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
     (void)hipGetLastError();

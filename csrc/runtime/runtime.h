@@ -83,6 +83,9 @@ bool is_device_pointer(const void *p);
 // Elements from which host-pointer array ops go to the GPU
 // (VELES_GPU_MIN_ELEMS, default 1 << 20).
 size_t gpu_min_elems();
+// Percent applied to the small-call host limits of the simd = 1 host API
+// (VELES_HOST_SMALL_SCALE, default 100; 0 sends every such call to the GPU).
+size_t host_small_scale();
 // Launch helper: grid size for a grid-stride elementwise kernel.
 unsigned elementwise_grid(size_t work_items, unsigned block);
 // Compute units of the current device (cached; 256 on MI355X), for sizing

@@ -8,6 +8,13 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
 
+# The simd = 1 host API keeps small calls on the host (a GPU round trip costs
+# more than the work).  The suite's small shapes are meant for the device
+# kernels, so the tests switch that policy off; tests/test_host_fast.py covers
+# the policy itself in child processes with the default environment.
+os.environ.setdefault("VELES_HOST_SMALL_SCALE", "0")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")

@@ -53,7 +53,7 @@ def test_handles_vs_brute(prefix, xlen, hlen, tol, corr):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("xlen,hlen", [(4096, 64), (20000, 333)])
+@pytest.mark.parametrize("xlen,hlen", [(16384, 64), (20000, 333)])
 def test_convolve_simd_gpu_direct_host_api(xlen, hlen):
     """Above VELES_HOST_MAX_MACS the simd=1 host API stages to the GPU
     direct kernel (smaller calls stay on the host reference by design)."""

@@ -1,0 +1,119 @@
+"""Vectorised host loops for calls too small for a GPU round trip
+(csrc/ref/host_fast.cpp) against the scalar host reference (`simd = 0`, `_na`).
+
+The calls below stay under VELES_HOST_MAX_MACS / VELES_GPU_MIN_ELEMS, so they run
+the host loops on a GPU box too.  Reference counterparts: the AVX loops of
+/root/reference/src/convolve.c:49-100 and src/wavelet.c:395-1555."""
+import numpy as np
+import pytest
+
+from veles.simd_amd import capi
+
+WAVELETS = [(0, o) for o in (2, 4, 6, 8, 12, 16, 20, 38, 76)] + \
+           [(1, o) for o in (6, 12, 18, 24, 30)] + [(2, o) for o in (4, 8, 16, 20)]
+
+
+def _rng(seed):
+    return np.random.default_rng(seed)
+
+
+@pytest.mark.parametrize("xlen,hlen", [
+    (1, 1), (7, 3), (3, 7), (64, 23), (23, 64),          # tap-by-tap accumulation
+    (200, 50), (1000, 50), (50, 1000),                    # register-blocked outputs
+    (512, 512), (24, 24), (63, 65), (64, 64), (65, 63), (129, 24), (700, 700)])
+@pytest.mark.parametrize("correlate", [False, True])
+def test_direct_matches_scalar_reference(xlen, hlen, correlate):
+    rng = _rng(xlen * 1000 + hlen)
+    x = rng.standard_normal(xlen).astype(np.float32)
+    h = rng.standard_normal(hlen).astype(np.float32)
+    fast = capi.convolve_simd(1, x, h, correlate)
+    slow = capi.convolve_simd(0, x, h, correlate)
+    want = np.convolve(x.astype(np.float64), h[::-1].astype(np.float64) if correlate
+                       else h.astype(np.float64))
+    assert fast.shape == slow.shape == want.shape
+    tol = 4e-6 * min(xlen, hlen) ** 0.5 * 8
+    np.testing.assert_allclose(fast, want, atol=tol)
+    np.testing.assert_allclose(fast, slow, atol=tol)
+
+
+@pytest.mark.parametrize("type_,order", WAVELETS)
+@pytest.mark.parametrize("ext", [0, 1, 2, 3])
+def test_dwt_matches_scalar_reference(type_, order, ext):
+    for n in (order + (order & 1), 64, 130, 512):
+        if n < order:
+            continue
+        src = _rng(n + order).standard_normal(n).astype(np.float32)
+        hi, lo = capi.wavelet_apply(type_, order, ext, src)
+        hi0, lo0 = capi.wavelet_apply(type_, order, ext, src, na=True)
+        np.testing.assert_allclose(hi, hi0, atol=2e-5)
+        np.testing.assert_allclose(lo, lo0, atol=2e-5)
+
+
+@pytest.mark.parametrize("type_,order", [(0, 4), (0, 8), (0, 16), (1, 12), (2, 6)])
+@pytest.mark.parametrize("ext", [0, 1, 2, 3])
+@pytest.mark.parametrize("level", [1, 2, 3, 5])
+def test_swt_matches_scalar_reference(type_, order, ext, level):
+    for n in (64, 257, 512):
+        src = _rng(n + level).standard_normal(n).astype(np.float32)
+        hi, lo = capi.stationary_wavelet_apply(type_, order, level, ext, src)
+        hi0, lo0 = capi.stationary_wavelet_apply(type_, order, level, ext, src, na=True)
+        np.testing.assert_allclose(hi, hi0, atol=2e-5)
+        np.testing.assert_allclose(lo, lo0, atol=2e-5)
+
+
+def _child(code, **env):
+    import os
+    import subprocess
+    import sys
+    e = dict(os.environ, **env)
+    e.pop("VELES_HOST_SMALL_SCALE", None)       # the shipped default policy
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout + r.stderr
+
+
+_SMALL_CALLS = r"""
+import numpy as np
+from veles.simd_amd import capi
+rng = np.random.default_rng(5)
+a = rng.standard_normal((37, 53)).astype(np.float32)
+b = rng.standard_normal((37, 53)).astype(np.float32)
+np.testing.assert_array_equal(capi.matrix_add(1, a, b, 53, 37), (a + b).ravel())
+np.testing.assert_array_equal(capi.matrix_sub(1, a, b, 53, 37), (a - b).ravel())
+m1 = rng.standard_normal((19, 45)).astype(np.float32)     # h1 x w1
+m2 = rng.standard_normal((45, 31)).astype(np.float32)     # w1 x w2
+got = capi.matrix_multiply(1, m1, m2, 45, 19, 31, 45).reshape(19, 31)
+np.testing.assert_allclose(got, m1.astype(np.float64) @ m2.astype(np.float64), atol=2e-5)
+m2t = np.ascontiguousarray(m2.T)                            # h2 x w2 = 31 x 45
+got = capi.matrix_multiply_transposed(1, m1, m2t, 45, 19, 45, 31).reshape(19, 31)
+np.testing.assert_allclose(got, m1.astype(np.float64) @ m2.astype(np.float64), atol=2e-5)
+x = rng.uniform(0.1, 3.0, 300).astype(np.float32)
+for name in ("sin_psv", "cos_psv", "exp_psv", "log_psv", "sqrt_psv"):
+    np.testing.assert_array_equal(capi.psv(name, 1, x), capi.psv(name, 0, x))
+print("small calls ok")
+"""
+
+
+def test_small_matrix_and_math_calls_run_host_loops():
+    """Default policy: the small simd = 1 calls give the host results (libm bit for bit)
+    and never report a GPU call in the level-2 log."""
+    out = _child(_SMALL_CALLS, VELES_LOG_LEVEL="2")
+    assert "small calls ok" in out
+    assert "done on GPU" not in out
+
+
+@pytest.mark.gpu
+def test_larger_calls_still_reach_the_gpu():
+    code = r"""
+import numpy as np
+from veles.simd_amd import capi
+a = np.ones((200, 200), np.float32)
+capi.matrix_add(1, a, a, 200, 200)
+capi.matrix_multiply(1, a, a, 200, 200, 200, 200)
+capi.psv("sin_psv", 1, np.ones(5000, np.float32))
+"""
+    out = _child(code, VELES_LOG_LEVEL="2")
+    for what in ("matrix_add", "matrix_multiply", "sin_psv"):
+        assert f"{what}: done on GPU" in out

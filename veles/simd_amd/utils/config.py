@@ -30,8 +30,11 @@ KNOBS = [
          "paths)", "csrc/runtime/runtime.cpp"),
     Knob("VELES_GPU_MIN_ELEMS", str(1 << 20), "host arrays of at least this many elements "
          "(x taps for wavelets) run on the GPU in the flag-less API", "csrc/runtime/runtime.cpp"),
-    Knob("VELES_HOST_MAX_MACS", str(1 << 17), "direct convolutions of host operands below "
-         "this many multiply-adds run on the host even with simd=1", "csrc/api/convolve.cpp"),
+    Knob("VELES_HOST_MAX_MACS", str(1 << 19), "convolutions of host operands (direct calls and handles) "
+         "below this many multiply-adds run on the host even with simd=1", "csrc/api/convolve.cpp"),
+    Knob("VELES_HOST_SMALL_SCALE", "100", "percent applied to the small-call limits below which "
+         "simd=1 matrix / math calls on host operands run host loops (0: always the GPU)",
+         "csrc/runtime/runtime.cpp"),
     Knob("VELES_SYNC_STAGE", "0", "1: stage host operands with synchronous copies (debug)",
          "csrc/runtime/runtime.cpp"),
     Knob("VELES_ZERO_COPY", "1", "0: stage every small host operand into device memory "
