@@ -902,11 +902,26 @@ __global__ __launch_bounds__((Plan<LOGM, EP>::TPS), (real_min_waves<LOGM, EP>())
 // partitions go by in groups of kFdlGroup whose P / Q (2 float4 each) stay in
 // registers while the lane walks the source blocks the group needs, so
 // every Z load (16 bytes) feeds up to 4 kFdlGroup complex multiply-adds.
-// Groups of 4 at 64 VGPRs: 0.38 / 0.94 ms for 8 / 25 partitions at 2^20 x 64
-// (about 5 TB/s of Z reads and Y writes); groups of 8 read less but run at
-// two waves per SIMD and lose 7-14 % (profiles/r3/conv/fdl.md).
+// Groups of 4: 0.38 / 0.94 ms for 8 / 25 partitions at 2^20 x 64 (about
+// 5 TB/s of Z reads and Y writes); groups of 8 read less but run at two waves
+// per SIMD and lose 7-14 % (profiles/r3/conv/fdl.md).  Kept as the A/B arm of
+// the LDS-staged kernel below (vs_tune_set("fdl_mac_lds", 0)).
 constexpr int kFdlTile = 16;
 constexpr int kFdlGroup = 4;
+
+// acc += P z + Q conj(zc), pq = (P.re, P.im, Q.re, Q.im): eight fused
+// multiply-adds straight into the accumulator.
+__device__ __forceinline__ void fdl_acc(float2 &acc, const float4 pq, const float2 z,
+                                        const float2 zc) {
+  acc.x = fmaf(pq.x, z.x, acc.x);
+  acc.y = fmaf(pq.x, z.y, acc.y);
+  acc.x = fmaf(-pq.y, z.y, acc.x);
+  acc.y = fmaf(pq.y, z.x, acc.y);
+  acc.x = fmaf(pq.z, zc.x, acc.x);
+  acc.y = fmaf(pq.w, zc.x, acc.y);
+  acc.x = fmaf(pq.w, zc.y, acc.x);
+  acc.y = fmaf(-pq.z, zc.y, acc.y);
+}
 
 struct FdlMac {
   const float2 *Z;   // [batch][nsrc][M]
@@ -948,10 +963,8 @@ __global__ __launch_bounds__(256) void fdl_mac_kernel(FdlMac a) {
       for (int pp = 0; pp < G; pp++) {
         const int o = i - (G - 1) + pp;
         if (o < 0 || o >= kFdlTile) continue;
-        acck[o] = fft::cadd(acck[o], fft::cadd(cmul(make_float2(pk[pp].x, pk[pp].y), zk),
-                                               fft::cmulc(make_float2(pk[pp].z, pk[pp].w), zm)));
-        accm[o] = fft::cadd(accm[o], fft::cadd(cmul(make_float2(pm[pp].x, pm[pp].y), zm),
-                                               fft::cmulc(make_float2(pm[pp].z, pm[pp].w), zk)));
+        fdl_acc(acck[o], pk[pp], zk, zm);
+        fdl_acc(accm[o], pm[pp], zm, zk);
       }
     }
   }
@@ -966,6 +979,92 @@ __global__ __launch_bounds__(256) void fdl_mac_kernel(FdlMac a) {
                                 reinterpret_cast<native2 *>(Y + static_cast<long long>(b0 + o) * a.m + km));
   }
 }
+
+// Spectral accumulation with the source spectra staged in LDS.  A workgroup
+// owns 64 bin pairs (k, M - k) of kFdlLdsTile consecutive output blocks of one
+// signal and walks the partitions in chunks of at most `pc_max`: the
+// kFdlLdsTile + chunk - 1 source blocks a chunk needs are read from memory
+// once into LDS (1 KiB per block), each wave accumulates kFdlLdsTile / 4
+// outputs, and a partition's P / Q pair is loaded once per wave for all of
+// them.  Against the register kernel above Z is read (tile + parts - 1) / tile
+// times instead of 1.19 times per group of 4 partitions.
+constexpr int kFdlLdsTile = 32;
+constexpr int kFdlLdsBins = 64;
+constexpr int kFdlLdsChunk = 32;  // (32 + 32 - 1) KiB of LDS, under the 64 KiB dynamic limit
+
+template <int PCMAX>
+__global__ __launch_bounds__(256, (PCMAX > 16 ? 2 : 3)) void fdl_mac_lds_kernel(FdlMac a) {
+  constexpr int pc_max = PCMAX;
+  extern __shared__ float2 zl[];  // [rows][128]: 64 bins k, then their 64 mirrors
+  constexpr int NB = kFdlLdsBins, OPT = kFdlLdsTile / 4;
+  const int t = threadIdx.x, jj = t & (NB - 1), sub = t >> 6;
+  const int half = a.m / 2, mask = a.m - 1;
+  const int j = blockIdx.x * NB + jj;
+  const bool live = j <= half;
+  const int k = live ? j : 0, km = live ? (a.m - j) & mask : 0;
+  const long long sig = blockIdx.z;
+  const int b0 = blockIdx.y * kFdlLdsTile;
+  const float2 *Z = a.Z + sig * a.nsrc * a.m;
+  const float4 *PQ = a.PQ + (a.pq_per_signal ? sig * a.parts * a.m : 0);
+  float2 acck[OPT], accm[OPT];
+#pragma unroll
+  for (int i = 0; i < OPT; i++) acck[i] = accm[i] = make_float2(0.f, 0.f);
+  for (int pc0 = 0; pc0 < a.parts; pc0 += pc_max) {
+    const int pcn = min(pc_max, a.parts - pc0);
+    const int rows = kFdlLdsTile + pcn - 1;
+    const int s0 = b0 - pc0 - (pcn - 1);  // row r holds source block s0 + r
+    if (pc0) __syncthreads();             // the previous chunk's readers are done
+    // every load of the chunk in flight before the first LDS store
+    constexpr int kLoads = (kFdlLdsTile + PCMAX - 1 + 1) / 2;  // two rows per pass of 256 lanes
+    float2 v[kLoads];
+    const int c = t & (2 * NB - 1);
+    const int jb = blockIdx.x * NB + (c & (NB - 1));
+    const int bin = c < NB ? jb : (a.m - jb) & mask;
+#pragma unroll
+    for (int u = 0; u < kLoads; u++) {
+      const int r = 2 * u + (t >> 7);
+      const int s = s0 + r;
+      v[u] = make_float2(0.f, 0.f);
+      if (r < rows && s >= 0 && s < a.nsrc && jb <= half) v[u] = Z[static_cast<long long>(s) * a.m + bin];
+    }
+#pragma unroll
+    for (int u = 0; u < kLoads; u++) {
+      const int r = 2 * u + (t >> 7);
+      if (r < rows) zl[r * 2 * NB + c] = v[u];
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int p = 0; p < pcn; p++) {
+      const float4 pk = PQ[static_cast<long long>(pc0 + p) * a.m + k];
+      const float4 pm = PQ[static_cast<long long>(pc0 + p) * a.m + km];
+#pragma unroll
+      for (int i = 0; i < OPT; i++) {
+        // output b0 + o through partition pc0 + p reads source b0 + o - pc0 - p
+        const int r = sub * OPT + i - p + (pcn - 1);
+        const float2 zk = zl[r * 2 * NB + jj], zm = zl[r * 2 * NB + NB + jj];
+        fdl_acc(acck[i], pk, zk, zm);
+        fdl_acc(accm[i], pm, zm, zk);
+      }
+    }
+  }
+  if (!live) return;
+  float2 *Y = a.Y + sig * a.nblk * a.m;
+#pragma unroll
+  for (int i = 0; i < OPT; i++) {
+    const int o = b0 + sub * OPT + i;
+    if (o >= a.nblk) break;
+    typedef float native2 __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(native2{acck[i].x, acck[i].y},
+                                reinterpret_cast<native2 *>(Y + static_cast<long long>(o) * a.m + k));
+    __builtin_nontemporal_store(native2{accm[i].x, accm[i].y},
+                                reinterpret_cast<native2 *>(Y + static_cast<long long>(o) * a.m + km));
+  }
+}
+
+// 0: register kernel (fdl_mac_kernel), 1: LDS-staged kernel.  vs_tune_set("fdl_mac_lds").
+thread_local int g_fdl_mac_lds = 1;
+// Partitions per LDS chunk: 0 = by partition count, or 8 / 16 / 32.  vs_tune_set("fdl_mac_chunk").
+thread_local int g_fdl_mac_chunk = 0;
 
 // ------------------------------------------ large FFT path (four-step)
 // z[p][n] = x[2p][n] + i x[2p+1][n] (zero padded to 2^logm)
@@ -1045,7 +1144,7 @@ thread_local int g_conv_real_all = 0;
 
 bool use_real(int logl);
 int fdl_part_taps();
-constexpr int kFdlMaxParts = 12;
+constexpr int kFdlMaxParts = 20;
 
 // Longest row one kernel launch sequence handles: the buffer-descriptor
 // loads and stores of the block kernels need every byte offset of a row in
@@ -1108,8 +1207,9 @@ int select(int64_t xlen, int hlen, int batch) {
   if (os_ok) return VS_CONV_OVERLAP_SAVE;
   // Long filter: uniformly partitioned overlap-save up to kFdlMaxParts
   // partitions (its spectral accumulation grows with the partition count:
-  // at 2^20 x 64, 8 partitions run 80 Gsamples/s, 25 run 50, the fused
-  // four-step transform 70 whatever the filter), else one padded transform
+  // at 2^20 x 64, 8 partitions run 100 Gsamples/s, 13 run 93, 20 run 73, 25
+  // run 66, the fused four-step transform 70 whatever the filter), else one
+  // padded transform
   // while it exists (vs_conv1d never fails for a valid shape).
   const int parts = (hlen + fdl_part_taps() - 1) / fdl_part_taps();
   return parts <= kFdlMaxParts || lm > fft::kMaxLog ? VS_CONV_OVERLAP_SAVE : VS_CONV_FFT;
@@ -1338,11 +1438,29 @@ vs_status run_fdl_t(int correlate, const float *x, int xlen, int64_t xs, const f
       hipLaunchKernelGGL((fdl_forward_kernel<LOGM, EP, false>), gf, dim3(PL::TPS), 0, s, a, Z, tw);
     FdlMac m{Z, PQ + (hs ? static_cast<size_t>(b0) * parts * M : 0), Y, nsrc, nblk, parts, M,
              hs != 0};
-    hipLaunchKernelGGL(fdl_mac_kernel,
-                       dim3((M / 2 + 1 + 255) / 256,
-                            static_cast<unsigned>((nblk + kFdlTile - 1) / kFdlTile),
-                            static_cast<unsigned>(nb)),
-                       dim3(256), 0, s, m);
+    if (g_fdl_mac_lds) {
+      // chunks of 8 partitions while that is all of them, else 16 (47 KiB of LDS, three
+      // workgroups per CU: 25 partitions run 67 Gsamples/s against 65 with chunks of 32
+      // and 58 with chunks of 8, profiles/r3/conv/fdl.md)
+      const int pc_max = g_fdl_mac_chunk ? g_fdl_mac_chunk
+                                         : parts <= 8 ? 8 : 16;
+      const size_t lds = static_cast<size_t>(kFdlLdsTile + pc_max - 1) * 2 * kFdlLdsBins * sizeof(float2);
+      const dim3 gm((M / 2 + 1 + kFdlLdsBins - 1) / kFdlLdsBins,
+                    static_cast<unsigned>((nblk + kFdlLdsTile - 1) / kFdlLdsTile),
+                    static_cast<unsigned>(nb));
+      if (pc_max == 8)
+        hipLaunchKernelGGL(fdl_mac_lds_kernel<8>, gm, dim3(256), lds, s, m);
+      else if (pc_max == 16)
+        hipLaunchKernelGGL(fdl_mac_lds_kernel<16>, gm, dim3(256), lds, s, m);
+      else
+        hipLaunchKernelGGL(fdl_mac_lds_kernel<kFdlLdsChunk>, gm, dim3(256), lds, s, m);
+    } else {
+      hipLaunchKernelGGL(fdl_mac_kernel,
+                         dim3((M / 2 + 1 + 255) / 256,
+                              static_cast<unsigned>((nblk + kFdlTile - 1) / kFdlTile),
+                              static_cast<unsigned>(nb)),
+                         dim3(256), 0, s, m);
+    }
     if (buf)
       hipLaunchKernelGGL((fdl_inverse_kernel<LOGM, EP, true>), gi, dim3(PL::TPS), 0, s, a, Y, tw);
     else
@@ -1629,6 +1747,16 @@ vs_status vs_tune_set(const char *key, int value) {
     conv::g_fdl_log = value;
     return VS_OK;
   }
+  if (std::strcmp(key, "fdl_mac_chunk") == 0) {
+    VS_REQUIRE(value == 0 || value == 8 || value == 16 || value == 32,
+               "fdl_mac_chunk must be 0, 8, 16 or 32");
+    conv::g_fdl_mac_chunk = value;
+    return VS_OK;
+  }
+  if (std::strcmp(key, "fdl_mac_lds") == 0) {
+    conv::g_fdl_mac_lds = value != 0;
+    return VS_OK;
+  }
   if (wav::tune(key, value)) return VS_OK;
   set_error("vs_tune_set: unknown key '%s'", key);
   return VS_ERR_INVALID;
@@ -1642,6 +1770,8 @@ void vs_tune_reset(void) {
   conv::g_conv_real = 1;
   conv::g_conv_real_all = 0;
   conv::g_fdl_log = 14;
+  conv::g_fdl_mac_lds = 1;
+  conv::g_fdl_mac_chunk = 0;
   conv::g_piece_log = 28;
   wav::tune_reset();
 }

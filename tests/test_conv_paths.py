@@ -206,12 +206,26 @@ def test_uniformly_partitioned_overlap_save(block_log, xlen, hlen, batch, per_si
         _check(xlen, hlen, batch, "overlap_save", corr, per_signal=per_signal)
 
 
-def test_partitioned_many_output_tiles():
-    """More output blocks than one accumulation tile (16) and more than four
-    partitions: every (tile, partition group) edge of fdl_mac_kernel."""
-    _check(8192 * 37 + 5, 8192 * 5 + 77, 2, "overlap_save", False)
+@pytest.mark.parametrize("lds", [1, 0])
+def test_partitioned_many_output_tiles(lds):
+    """More output blocks than one accumulation tile (32 in the LDS-staged
+    kernel, 16 in the register kernel) and more than four partitions: every
+    (tile, partition group) edge of both accumulation kernels."""
+    with _knob("fdl_mac_lds", lds, 1):
+        _check(8192 * 37 + 5, 8192 * 5 + 77, 2, "overlap_save", False)
+        with _knob("fdl_block_log", 13, 14):
+            _check(4096 * 41 + 3, 4096 * 9 + 1, 1, "overlap_save", True)
+            _check(4096 * 70 + 3, 4096 * 2 + 1, 2, "overlap_save", False, per_signal=True)
+
+
+def test_partitioned_more_partitions_than_one_lds_chunk():
+    """40 and 67 partitions of 4096 taps: the LDS-staged accumulation walks them
+    in chunks of 32 (two and three chunks), against the register kernel."""
     with _knob("fdl_block_log", 13, 14):
-        _check(4096 * 41 + 3, 4096 * 9 + 1, 1, "overlap_save", True)
+        for hlen in (4096 * 39 + 11, 4096 * 66 + 4095):
+            _check(4096 * 45 + 9, hlen, 2, "overlap_save", False)
+            with _knob("fdl_mac_lds", 0, 1):
+                _check(4096 * 45 + 9, hlen, 1, "overlap_save", True)
 
 
 def test_partitioned_plan_matches_call():
@@ -297,13 +311,16 @@ def test_rows_beyond_2p31(n, hlen, algo):
 def test_select_long_filter_overlap_save():
     """Filters whose L = 32768 block is >= 28 % useful run single-block
     overlap-save (h = 20000: 144 vs 73 Gsamples/s for the fused four-step
-    FFT); longer ones the uniformly partitioned path up to 12 partitions of
-    8192 taps (h = 65536: 89 vs 70), then the FFT (profiles/r3/conv/fdl.md)."""
+    FFT); longer ones the uniformly partitioned path up to 20 partitions of
+    8192 taps (h = 65536: 100 vs 70, h = 163840: 73 vs 70), then the FFT
+    (profiles/r3/conv/fdl.md)."""
     from veles.simd_amd import _lib
     lib = _lib.lib()
     assert lib.vs_conv1d_select(1 << 20, 20000, 64) == 3
     assert lib.vs_conv1d_select(1 << 20, 30000, 64) == 3
     assert lib.vs_conv1d_select(1 << 20, 98304, 64) == 3
+    assert lib.vs_conv1d_select(1 << 20, 163840, 64) == 3
+    assert lib.vs_conv1d_select(1 << 20, 163841, 64) == 2
     assert lib.vs_conv1d_select(1 << 20, 200000, 64) == 2
     assert lib.vs_conv1d_select(1 << 27, 200000, 1) == 3   # beyond the largest transform
     _check(200000, 20000, 2, "auto", False)

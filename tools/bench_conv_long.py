@@ -2,7 +2,8 @@
 """Long-filter convolution throughput (Msamples/s of input), x = XLEN x BATCH:
 explicit overlap-save (the partitioned path past one block), the whole-signal
 FFT and auto, shared and per-signal filters.  Run once per library
-(VELES_SIMD_LIB) for an A/B.  HLENS=65536,200000 XLEN=1048576 BATCH=64."""
+(VELES_SIMD_LIB) for an A/B.  HLENS=65536,200000 XLEN=1048576 BATCH=64
+[TUNE=fdl_mac_lds=0,...  vs_tune_set knobs for the whole run]."""
 import json
 import os
 import statistics
@@ -19,6 +20,9 @@ def main():
     batch = int(os.environ.get("BATCH", 64))
     rounds = int(os.environ.get("ROUNDS", 4))
     hlens = [int(v) for v in os.environ.get("HLENS", "65536,200000").split(",")]
+    for kv in [kv for kv in os.environ.get("TUNE", "").split(",") if kv]:
+        name, value = kv.split("=")
+        _lib.call("vs_tune_set", name.encode(), int(value))
     x = torch.randn(batch, xlen, device="cuda")
     res = {}
     for hlen in hlens:
