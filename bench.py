@@ -171,7 +171,16 @@ def main():
         secondary["sgemm_bf16x3_max_abs_err"] = err3
 
     # ----------------------------------------------------------------- conv
-    if not args.no_conv and hasattr(lib, "vs_conv1d"):
+    # A failure in a secondary section (it would be the same on every rank: a
+    # shape or API error, not a lost rank) is recorded instead of losing the
+    # headline line.
+    def _secondary(name, fn):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001
+            secondary[name + "_error"] = f"{type(e).__name__}: {e}"[:300]
+
+    def _conv_section():
         x = torch.randn((CONV_BATCH, CONV_LEN), device="cuda", generator=g)
         h = torch.randn((CONV_H,), device="cuda", generator=g)
         ylen = CONV_LEN + CONV_H - 1
@@ -246,6 +255,9 @@ def main():
                                   max(0, algo - 1)]},
         })
 
+    if not args.no_conv and hasattr(lib, "vs_conv1d"):
+        _secondary("conv1d", _conv_section)
+
     # ------------------------------------- benchmark configs with communication
     # Config 5 (row-split batched SGEMM 8192^2 x 64, RCCL all-gather of the C
     # row blocks over xGMI, overlapped with the next matrix's GEMM: every rank
@@ -253,7 +265,7 @@ def main():
     # 34-48 GiB per GPU) and config 4
     # (SWT db8 x 8 levels over 65536 x 1024 signals, batch sharded over the
     # ranks).  Both run under the same barrier / max-over-ranks clock.
-    if not args.no_comm:
+    def _rowsplit_section():
         from veles.simd_amd import parallel
         rs_n, rs_batch = 8192, 64
         m_loc = rs_n // world
@@ -283,7 +295,10 @@ def main():
         })
         del a_loc, bmat, cfull
 
+    def _swt_section():
+        from veles.simd_amd import parallel
         total, sn, levels = 65536, 1024, 8
+        ga = torch.Generator(device="cuda").manual_seed(78 + rank)
         s0, s1 = parallel.shard_range(total, world, rank)
         xs = torch.randn(s1 - s0, sn, device="cuda", generator=ga)
         hi = torch.empty(s1 - s0, levels, sn, device="cuda")
@@ -305,6 +320,10 @@ def main():
                               "len": sn, "parallelism": f"dp{world}"},
         })
         del xs, hi, lo
+
+    if not args.no_comm:
+        _secondary("rowsplit", _rowsplit_section)
+        _secondary("swt_dp", _swt_section)
 
     base = _baseline()
     vs_base = None

@@ -1205,8 +1205,7 @@ vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,
     const float *in = src;
     int64_t n = len64, in_stride = len64, off = 0;
     int done = 0, pass = 0;
-    bool tiled = g_dwt_vec != 0;
-    while (tiled && done < levels) {
+    while (g_dwt_vec != 0 && done < levels) {
       const int64_t tile = std::min<int64_t>(g_dwt_tile, n);
       const int lf = dwt_tile_levels(order, tile, levels - done);
       const int64_t nout = n >> lf;
@@ -1219,10 +1218,7 @@ vs_status vs_dwt_multilevel(int type, int order, int levels, int ext,
       DwtTileArgs a{in, in_stride, n, out, len64, off, lo, last ? len64 : nout,
                     lf, ext, 0, 0, 0, 0};
       vs_status st;
-      if (!dwt_tiled(t, a, batch, s, &st)) {
-        tiled = false;  // no instantiation for this filter length
-        break;
-      }
+      if (!dwt_tiled(t, a, batch, s, &st)) break;  // no instantiation for this filter length
       VS_TRY(st);
       in = lo;
       in_stride = nout;
