@@ -9,6 +9,13 @@
 using vs::Staged;
 
 namespace {
+// Planes / arrays this small stay on the host even with simd = 1 (a GPU
+// round trip costs 14-18 us; the host loops pass 16 K elements in less).
+constexpr size_t kSmallElems = 16384;
+bool small(int w, int h, std::initializer_list<const void *> ptrs) {
+  return vs::api::host_small(static_cast<size_t>(w) * h, kSmallElems, ptrs);
+}
+
 size_t plane_bytes(int stride, int w, int h, size_t elem) {
   return (static_cast<size_t>(h - 1) * stride + w) * elem;
 }
@@ -21,7 +28,7 @@ void minmax2D(int simd, const uint8_t *src, int stride, int w, int h,
   if (!src || w <= 0 || h <= 0 || stride < w)
     vs::fatal("minmax2D: invalid arguments");
   if (!mn && !mx) return;
-  if (!vs::api::use_gpu_simd(simd, "minmax2D")) {
+  if (!vs::api::use_gpu_simd(simd, "minmax2D") || small(w, h, {src})) {
     vs::ref::minmax2d(src, stride, w, h, mn, mx);
     return;
   }
@@ -42,7 +49,7 @@ void normalize2D_minmax(int simd, uint8_t mn, uint8_t mx, const uint8_t *src,
                         int sstride, int w, int h, float *dst, int dstride) {
   if (!src || !dst || w <= 0 || h <= 0 || sstride < w || dstride < w || mn > mx)
     vs::fatal("normalize2D_minmax: invalid arguments");
-  if (!vs::api::use_gpu_simd(simd, "normalize2D_minmax")) {
+  if (!vs::api::use_gpu_simd(simd, "normalize2D_minmax") || small(w, h, {src, dst})) {
     vs::ref::normalize2d_minmax(mn, mx, src, sstride, w, h, dst, dstride);
     return;
   }
@@ -62,7 +69,7 @@ void normalize2D(int simd, const uint8_t *src, int sstride, int w, int h,
                  float *dst, int dstride) {
   if (!src || !dst || w <= 0 || h <= 0 || sstride < w || dstride < w)
     vs::fatal("normalize2D: invalid arguments");
-  if (!vs::api::use_gpu_simd(simd, "normalize2D")) {
+  if (!vs::api::use_gpu_simd(simd, "normalize2D") || small(w, h, {src, dst})) {
     uint8_t mn, mx;
     vs::ref::minmax2d(src, sstride, w, h, &mn, &mx);
     vs::ref::normalize2d_minmax(mn, mx, src, sstride, w, h, dst, dstride);
@@ -86,7 +93,7 @@ void normalize2D(int simd, const uint8_t *src, int sstride, int w, int h,
 void minmax1D(int simd, const float *src, int n, float *mn, float *mx) {
   if (!src || n <= 0) vs::fatal("minmax1D: invalid arguments");
   if (!mn && !mx) return;
-  if (!vs::api::use_gpu_simd(simd, "minmax1D")) {
+  if (!vs::api::use_gpu_simd(simd, "minmax1D") || small(n, 1, {src})) {
     vs::ref::minmax1d(src, n, mn, mx);
     return;
   }

@@ -19,7 +19,10 @@ void detect_peaks(int simd, const float *data, size_t size, ExtremumType type,
     vs::fatal("detect_peaks: invalid arguments (size=%zu)", size);
   *results = nullptr;
   *resultsLength = 0;
-  if (!vs::api::use_gpu_simd(simd, "detect_peaks")) {
+  // short arrays stay on the host: two GPU round trips (count, then emit)
+  // cost more than the scan
+  if (!vs::api::use_gpu_simd(simd, "detect_peaks") ||
+      vs::api::host_small(size, 16384, {data})) {
     vs::ref::detect_peaks(data, size, type, results, resultsLength);
     return;
   }

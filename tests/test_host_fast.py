@@ -89,6 +89,21 @@ np.testing.assert_allclose(got, m1.astype(np.float64) @ m2.astype(np.float64), a
 m2t = np.ascontiguousarray(m2.T)                            # h2 x w2 = 31 x 45
 got = capi.matrix_multiply_transposed(1, m1, m2t, 45, 19, 45, 31).reshape(19, 31)
 np.testing.assert_allclose(got, m1.astype(np.float64) @ m2.astype(np.float64), atol=2e-5)
+import ctypes
+img = rng.integers(0, 256, (40, 50), dtype=np.uint8)
+mn, mx = ctypes.c_uint8(), ctypes.c_uint8()
+capi.fn("minmax2D")(1, capi.p(img), 50, 50, 40, ctypes.byref(mn), ctypes.byref(mx))
+assert (mn.value, mx.value) == (img.min(), img.max())
+n1, n0 = np.empty((40, 50), np.float32), np.empty((40, 50), np.float32)
+capi.fn("normalize2D")(1, capi.p(img), 50, 50, 40, capi.p(n1), 50)
+capi.fn("normalize2D")(0, capi.p(img), 50, 50, 40, capi.p(n0), 50)
+np.testing.assert_array_equal(n1, n0)
+sig = rng.standard_normal(5000).astype(np.float32)
+p1, p0 = capi.detect_peaks(1, sig, 3), capi.detect_peaks(0, sig, 3)
+assert len(p1) == len(p0) > 100 and p1 == p0
+fmn, fmx = ctypes.c_float(), ctypes.c_float()
+capi.fn("minmax1D")(1, capi.p(sig), sig.size, ctypes.byref(fmn), ctypes.byref(fmx))
+assert (fmn.value, fmx.value) == (sig.min(), sig.max())
 x = rng.uniform(0.1, 3.0, 300).astype(np.float32)
 for name in ("sin_psv", "cos_psv", "exp_psv", "log_psv", "sqrt_psv"):
     np.testing.assert_array_equal(capi.psv(name, 1, x), capi.psv(name, 0, x))
