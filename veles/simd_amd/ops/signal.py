@@ -264,7 +264,8 @@ def _(X, n):
 # -------------------------------------------------------------- wavelets
 DAUBECHIES, COIFLET, SYMLET = 0, 1, 2
 PERIODIC, MIRROR, CONSTANT, ZERO = 0, 1, 2, 3
-_FAMILY = {"daubechies": 0, "db": 0, "coiflet": 1, "coif": 1, "symlet": 2, "sym": 2}
+_FAMILY = {"daubechies": 0, "db": 0, "coiflet": 1, "coiflets": 1, "coif": 1,
+           "symlet": 2, "symlets": 2, "sym": 2}
 _EXT = {"periodic": 0, "mirror": 1, "constant": 2, "zero": 3}
 
 
