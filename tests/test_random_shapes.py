@@ -144,3 +144,45 @@ def test_elementwise_reduce_peaks_random_sizes(seed):
         wd = int(rng.integers(1, 300))
         img = torch.from_numpy(rng.integers(0, 256, (h, wd), dtype=np.uint8))
         assert torch.allclose(ops.normalize2d(img.cuda()).cpu(), ops.normalize2d(img), atol=1e-6)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_host_c_api_random_shapes(seed):
+    """The reference-compatible host API (host pointers staged through the
+    runtime) against simd = 0 / numpy on random shapes: small operands in the
+    pinned arena, large ones through device staging."""
+    from veles.simd_amd import capi
+    rng = np.random.default_rng(5000 + seed)
+    for case in range(12):
+        xlen, hlen = _loguniform(rng, 4, 60000), _loguniform(rng, 1, 3000)
+        print(f"capi case {seed}/{case}: conv x={xlen} h={hlen}", flush=True)
+        x = rng.standard_normal(xlen).astype(np.float32)
+        h = rng.standard_normal(hlen).astype(np.float32)
+        for corr in (False, True):
+            want = np.convolve(x.astype(np.float64), (h[::-1] if corr else h).astype(np.float64))
+            got = capi.convolve_simd(1, x, h, corr)
+            tol = 1.5e-5 * np.sqrt(min(xlen, hlen)) * np.abs(x).max() * np.abs(h).max() + 1e-4
+            assert np.abs(got - want).max() <= tol, ("convolve_simd", xlen, hlen, corr)
+            res, _ = capi.run_handle("cross_correlate" if corr else "convolve", x, h)
+            assert np.abs(res - want).max() <= tol, ("handle", xlen, hlen, corr)
+        w1, h1, w2 = (_loguniform(rng, 1, 700) for _ in range(3))
+        print(f"capi case {seed}/{case}: matmul {h1}x{w1} . {w1}x{w2}", flush=True)
+        a = rng.uniform(-1, 1, (h1, w1)).astype(np.float32)
+        b = rng.uniform(-1, 1, (w1, w2)).astype(np.float32)
+        ref = a.astype(np.float64) @ b.astype(np.float64)
+        got = capi.matrix_multiply(1, a, b, w1, h1, w2, w1).reshape(h1, w2)
+        assert np.abs(got - ref).max() <= 2e-6 * w1 + 1e-6
+        bt = np.ascontiguousarray(b.T)
+        got = capi.matrix_multiply_transposed(1, a, bt, w1, h1, w1, w2).reshape(h1, w2)
+        assert np.abs(got - ref).max() <= 2e-6 * w1 + 1e-6
+        c = rng.uniform(-1, 1, (h1, w1)).astype(np.float32)
+        assert np.array_equal(capi.matrix_add(1, a, c, w1, h1), (a + c).ravel())
+        assert np.array_equal(capi.matrix_sub(1, a, c, w1, h1), (a - c).ravel())
+        n = _loguniform(rng, 3, 400000)
+        v = rng.uniform(0.05, 6.0, n).astype(np.float32)
+        for name, ref_fn in (("sin_psv", np.sin), ("exp_psv", np.exp), ("log_psv", np.log)):
+            got = capi.psv(name, 1, v).astype(np.float64)
+            want = ref_fn(v.astype(np.float64))
+            assert (np.abs(got - want) <= 4e-7 * np.abs(want) + 5e-7).all(), (name, n)
+        sig = rng.standard_normal(n).astype(np.float32)
+        assert capi.detect_peaks(1, sig, 3) == capi.detect_peaks(0, sig, 3)
