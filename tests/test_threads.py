@@ -1,0 +1,72 @@
+"""The host C API called from several host threads at once (ctypes releases the
+GIL for the duration of a call): every thread has its own staging arena, scratch
+vectors and error slot, the device work shares the library stream.  Runs on the
+host paths without a GPU and through the GPU paths on a GPU box (the larger
+shapes below are past every small-call limit).  The reference is reentrant by
+construction (pure functions over caller memory, /root/reference/src/convolve.c:49-100)."""
+import threading
+
+import numpy as np
+import pytest
+
+from veles.simd_amd import capi
+
+
+def _work(seed, rounds, errors):
+    try:
+        rng = np.random.default_rng(seed)
+        x = rng.standard_normal(3000 + 17 * seed).astype(np.float32)
+        h = rng.standard_normal(90 + seed).astype(np.float32)
+        xl = rng.standard_normal(40000 + 1001 * seed).astype(np.float32)
+        hl = rng.standard_normal(700 + 3 * seed).astype(np.float32)
+        a = rng.uniform(-1, 1, (64 + seed, 96)).astype(np.float32)
+        b = rng.uniform(-1, 1, (96, 80 + seed)).astype(np.float32)
+        big = rng.uniform(-1, 1, (200, 300)).astype(np.float32)
+        v = rng.uniform(0.1, 5.0, 5000 + seed).astype(np.float32)
+        sig = rng.standard_normal(30000 + seed).astype(np.float32)
+        src = rng.standard_normal(512).astype(np.float32)
+        want = {
+            "conv": np.convolve(x.astype(np.float64), h.astype(np.float64)),
+            "convl": np.convolve(xl.astype(np.float64), hl.astype(np.float64)),
+            "mm": a.astype(np.float64) @ b.astype(np.float64),
+            "add": (big + big).ravel(),
+            "exp": np.exp(v.astype(np.float64)),
+            "peaks": capi.detect_peaks(0, sig, 3),
+            "dwt": capi.wavelet_apply(0, 8, 0, src, na=True),
+        }
+        for _ in range(rounds):
+            assert np.abs(capi.convolve_simd(1, x, h) - want["conv"]).max() < 2e-3
+            assert np.abs(capi.convolve_simd(1, xl, hl) - want["convl"]).max() < 2e-2
+            res, _ = capi.run_handle("convolve", xl, hl)
+            assert np.abs(res - want["convl"]).max() < 2e-2
+            got = capi.matrix_multiply(1, a, b, 96, a.shape[0], b.shape[1], 96)
+            assert np.abs(got.reshape(want["mm"].shape) - want["mm"]).max() < 2e-4
+            assert np.array_equal(capi.matrix_add(1, big, big, 300, 200), want["add"])
+            got = capi.psv("exp_psv", 1, v).astype(np.float64)
+            assert (np.abs(got - want["exp"]) <= 4e-7 * want["exp"]).all()
+            assert capi.detect_peaks(1, sig, 3) == want["peaks"]
+            hi, lo = capi.wavelet_apply(0, 8, 0, src)
+            assert np.abs(hi - want["dwt"][0]).max() < 1e-5
+            assert np.abs(lo - want["dwt"][1]).max() < 1e-5
+    except BaseException as e:  # noqa: BLE001
+        errors.append((seed, repr(e)))
+
+
+def _run(nthreads, rounds):
+    errors = []
+    threads = [threading.Thread(target=_work, args=(i, rounds, errors)) for i in range(nthreads)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in threads), "a worker thread did not finish"
+    assert not errors, errors
+
+
+def test_host_api_from_many_threads_host_paths():
+    _run(8, 5)
+
+
+@pytest.mark.gpu
+def test_host_api_from_many_threads_gpu_paths():
+    _run(8, 10)
