@@ -439,6 +439,116 @@ def wavedec(x, family="daubechies", order=8, levels=1, ext="periodic"):
     return _wavedec(x, _fam(family), order, levels, _ext(ext))
 
 
+# ---------------------------------------------------- wavelet gradients
+# The transforms are linear in x: out = A x with A built from the filter taps
+# and the boundary extension, so grad_x = A^T grad_out.  A^T of one level is a
+# full convolution of the band gradients with the (dilated / upsampled) taps
+# -- the conv1d op, HIP kernels on the GPU -- followed by folding the part that
+# fell on the extension back onto the samples it was copied from.
+def _fold_extension(ge: torch.Tensor, n: int, ext: int) -> torch.Tensor:
+    gx = ge[..., :n].clone()
+    tail = ge[..., n:]
+    m = tail.shape[-1]
+    if m == 0 or ext == ZERO:
+        return gx
+    t = torch.arange(m, device=ge.device)
+    if ext == PERIODIC:
+        idx = t % n
+    elif ext == MIRROR:
+        idx = n - 1 - (t % n)
+    else:
+        idx = torch.full((m,), n - 1, device=ge.device)
+    return gx.index_add_(-1, idx, tail)
+
+
+def _bank(family: int, order: int, device):
+    lp = wavelet_filter(family, order)
+    return _qmf(lp).to(device), lp.to(device)
+
+
+def _dilate(f: torch.Tensor, dil: int) -> torch.Tensor:
+    if dil == 1:
+        return f
+    fd = f.new_zeros((f.shape[0] - 1) * dil + 1)
+    fd[::dil] = f
+    return fd
+
+
+def _swt_level_adjoint(g_hi, g_lo, hp, lp, dil: int, ext: int):
+    """Gradient of one stationary level (taps dilated by `dil`) to its input."""
+    n = g_hi.shape[-1]
+    ge = (_conv1d(g_hi.contiguous(), _dilate(hp, dil), 0, False) +
+          _conv1d(g_lo.contiguous(), _dilate(lp, dil), 0, False))
+    return _fold_extension(ge, n, ext)
+
+
+def _dwt_level_adjoint(g_hi, g_lo, hp, lp, ext: int, n: int):
+    """Gradient of one decimated level (bands of length n // 2) to its input
+    of length n."""
+    half = g_hi.shape[-1]
+    up = g_hi.new_zeros((2, *g_hi.shape[:-1], max(2 * half - 1, 1)))
+    up[0][..., ::2] = g_hi
+    up[1][..., ::2] = g_lo
+    ge = _conv1d(up[0], hp, 0, False) + _conv1d(up[1], lp, 0, False)
+    if ge.shape[-1] < n:
+        ge = torch.nn.functional.pad(ge, (0, n - ge.shape[-1]))
+    return _fold_extension(ge, n, ext)
+
+
+def _wavelet_setup(ctx, inputs, output):
+    ctx.params = tuple(inputs[1:])
+    ctx.lead = inputs[0].shape[:-1]
+    ctx.n = inputs[0].shape[-1]
+
+
+def _dwt_backward(ctx, g):
+    family, order, ext = ctx.params
+    hp, lp = _bank(family, order, g.device)
+    gr = g.reshape(2, -1, ctx.n // 2).float()
+    gx = _dwt_level_adjoint(gr[0], gr[1], hp, lp, ext, ctx.n)
+    return gx.reshape(*ctx.lead, ctx.n), None, None, None
+
+
+def _swt_level_backward(ctx, g):
+    family, order, level, ext = ctx.params
+    hp, lp = _bank(family, order, g.device)
+    gr = g.reshape(2, -1, ctx.n).float()
+    gx = _swt_level_adjoint(gr[0], gr[1], hp, lp, 1 << (level - 1), ext)
+    return gx.reshape(*ctx.lead, ctx.n), None, None, None, None
+
+
+def _swt_backward(ctx, g):
+    family, order, levels, ext = ctx.params
+    hp, lp = _bank(family, order, g.device)
+    gr = g.reshape(-1, levels + 1, ctx.n).float()
+    cur = gr[:, levels]
+    for lvl in range(levels - 1, -1, -1):   # the low band of level l feeds level l + 1
+        cur = _swt_level_adjoint(gr[:, lvl], cur, hp, lp, 1 << lvl, ext)
+    return cur.reshape(*ctx.lead, ctx.n), None, None, None, None
+
+
+def _wavedec_backward(ctx, g):
+    family, order, levels, ext = ctx.params
+    hp, lp = _bank(family, order, g.device)
+    gr = g.reshape(-1, ctx.n).float()
+    # rows are [hi_1 | hi_2 | ... | hi_L | lo_L]
+    starts, off, length = [], 0, ctx.n
+    for _ in range(levels):
+        length //= 2
+        starts.append((off, length))
+        off += length
+    cur = gr[:, off:off + length]
+    for off_l, len_l in reversed(starts):
+        cur = _dwt_level_adjoint(gr[:, off_l:off_l + len_l], cur, hp, lp, ext, 2 * len_l)
+    return cur.reshape(*ctx.lead, ctx.n), None, None, None, None
+
+
+_dwt.register_autograd(_dwt_backward, setup_context=_wavelet_setup)
+_swt_level.register_autograd(_swt_level_backward, setup_context=_wavelet_setup)
+_swt.register_autograd(_swt_backward, setup_context=_wavelet_setup)
+_wavedec.register_autograd(_wavedec_backward, setup_context=_wavelet_setup)
+
+
 # ----------------------------------------------------------------- peaks
 MAXIMUM, MINIMUM, BOTH = 1, 2, 3
 
