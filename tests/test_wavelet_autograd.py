@@ -100,3 +100,40 @@ def test_wavelet_module_passes_gradient_upstream():
     out = feats(lin(torch.randn(4, 128)))
     out.sum().backward()
     assert lin.weight.grad is not None and lin.weight.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("n", [8, 256, 4096])
+def test_fft_gradients(device, n):
+    """veles::fft / rfft / irfft against autograd through torch.fft in float64
+    (the unnormalised conventions of the library, FFTF's: reference
+    src/convolve.c:253-290)."""
+    torch.manual_seed(n)
+    z0 = torch.randn(3, n, 2)
+    for inverse in (False, True):
+        z = z0.to(device).requires_grad_()
+        zr = z0.double().requires_grad_()
+        c = torch.view_as_complex(zr)
+        ref = torch.view_as_real(torch.fft.ifft(c) * n if inverse else torch.fft.fft(c))
+        _compare(ops.fft(z, inverse), ref, z, zr, 2e-5 * n ** 0.5)
+    x0 = torch.randn(3, n)
+    x = x0.to(device).requires_grad_()
+    xr = x0.double().requires_grad_()
+    _compare(ops.rfft(x), torch.view_as_real(torch.fft.rfft(xr)), x, xr, 2e-5 * n ** 0.5)
+    X0 = torch.randn(3, n // 2 + 1, 2)
+    X0[:, 0, 1] = 0
+    X0[:, -1, 1] = 0
+    X = X0.to(device).requires_grad_()
+    Xr = X0.double().requires_grad_()
+    ref = torch.fft.irfft(torch.view_as_complex(Xr), n=n) * n
+    torch.manual_seed(2)
+    w = torch.randn(3, n, dtype=torch.float64)
+    g, = torch.autograd.grad((ops.irfft(X, n).double().cpu() * w).sum(), X)
+    g_ref, = torch.autograd.grad((ref * w).sum(), Xr)
+    # torch leaves the gradient of the ignored imaginary parts of the DC and
+    # Nyquist bins unspecified; compare everything else
+    g, g_ref = g.double().cpu().clone(), g_ref.clone()
+    for t in (g, g_ref):
+        t[:, 0, 1] = 0
+        t[:, -1, 1] = 0
+    assert (g - g_ref).abs().max() <= 2e-5 * n ** 0.5 * max(1.0, g_ref.abs().max().item())

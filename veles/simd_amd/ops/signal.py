@@ -261,6 +261,27 @@ def _(X, n):
     return X.new_empty((*X.shape[:-2], n))
 
 
+# Gradients of the transforms (real pairs (re, im) as the variables): the
+# adjoint of the unnormalised DFT is the unnormalised DFT of the other sign;
+# the half spectra of rfft / irfft count their interior bins twice.
+def _half_weights(g: torch.Tensor, interior: float) -> torch.Tensor:
+    w = g.new_full((g.shape[-2], 1), interior)
+    w[0] = w[-1] = 1.0
+    out = g * w
+    out[..., 0, 1] = 0.0    # the DC and Nyquist bins of a real signal are real
+    out[..., -1, 1] = 0.0
+    return out
+
+
+fft.register_autograd(lambda ctx, g: (fft(g.contiguous(), not ctx.inverse), None),
+                      setup_context=lambda ctx, inputs, output: setattr(ctx, "inverse", inputs[1]))
+rfft.register_autograd(
+    lambda ctx, g: irfft(_half_weights(g, 0.5), ctx.n),
+    setup_context=lambda ctx, inputs, output: setattr(ctx, "n", inputs[0].shape[-1]))
+irfft.register_autograd(lambda ctx, g: (_half_weights(rfft(g.contiguous()), 2.0), None),
+                        setup_context=lambda ctx, inputs, output: None)
+
+
 # -------------------------------------------------------------- wavelets
 DAUBECHIES, COIFLET, SYMLET = 0, 1, 2
 PERIODIC, MIRROR, CONSTANT, ZERO = 0, 1, 2, 3
