@@ -1,6 +1,6 @@
-"""Gradients of the wavelet ops (veles::dwt, swt_level, swt, wavedec): the
-registered backward (adjoint filter bank: conv1d op + extension fold) against
-torch autograd through a plain float64 formulation of the same transform
+"""Gradients of the custom ops: the registered backward of the wavelet ops
+(adjoint filter bank: conv1d op + extension fold), the transforms and the
+elementwise ops against torch autograd through a plain float64 formulation
 (reference definitions: /root/reference/src/wavelet.c:271-382)."""
 import pytest
 import torch
@@ -137,3 +137,49 @@ def test_fft_gradients(device, n):
         t[:, 0, 1] = 0
         t[:, -1, 1] = 0
     assert (g - g_ref).abs().max() <= 2e-5 * n ** 0.5 * max(1.0, g_ref.abs().max().item())
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_elementwise_gradients(device):
+    """Every differentiable elementwise op against torch autograd of the same
+    formula in float64."""
+    torch.manual_seed(3)
+    n = 2048
+    a0, b0 = torch.rand(n) * 2 + 0.5, torch.rand(n) * 2 + 0.5
+
+    def check(fn_op, fn_ref, *inputs0, tol=2e-5):
+        ins = [t.to(device).requires_grad_() for t in inputs0]
+        refs = [t.double().requires_grad_() for t in inputs0]
+        out, ref = fn_op(*ins), fn_ref(*refs)
+        outs = out if isinstance(out, (tuple, list)) else [out]
+        rfs = ref if isinstance(ref, (tuple, list)) else [ref]
+        ws = [torch.randn(r.shape, dtype=torch.float64) for r in rfs]
+        loss = sum((o.double().cpu() * w).sum() for o, w in zip(outs, ws))
+        loss_ref = sum((r * w).sum() for r, w in zip(rfs, ws))
+        gs = torch.autograd.grad(loss, ins)
+        gr = torch.autograd.grad(loss_ref, refs)
+        for g, r in zip(gs, gr):
+            assert (g.double().cpu() - r).abs().max() <= tol * max(1.0, r.abs().max().item())
+
+    check(ops.add, torch.add, a0, b0)
+    check(ops.sub, torch.sub, a0, b0)
+    check(ops.mul, torch.mul, a0, b0)
+    check(lambda x: ops.affine(x, 1.7, -0.3), lambda x: x * 1.7 - 0.3, a0)
+    check(lambda x, y: ops.saxpy(0.6, x, y), lambda x, y: 0.6 * x + y, a0, b0)
+    for fn in ("sin", "cos", "exp", "log", "sqrt"):
+        check(lambda x: ops.math(x, fn), getattr(torch, fn), a0)
+    check(ops.pow, torch.pow, a0, b0, tol=1e-4)
+    check(ops.sincos, lambda x: (torch.sin(x), torch.cos(x)), a0)
+    check(ops.sum_all, torch.sum, a0)
+
+    def cmul_ref(conj):
+        def f(a, b):
+            ca = torch.view_as_complex(a.reshape(-1, 2))
+            cb = torch.view_as_complex(b.reshape(-1, 2))
+            return torch.view_as_real(ca * (cb.conj() if conj else cb)).reshape(-1)
+        return f
+    check(lambda a, b: ops.complex_multiply(a, b), cmul_ref(False), a0, b0)
+    check(lambda a, b: ops.complex_multiply(a, b, True), cmul_ref(True), a0, b0)
+    check(ops.complex_conjugate,
+          lambda a: torch.view_as_real(torch.view_as_complex(a.reshape(-1, 2)).conj().resolve_conj()).reshape(-1),
+          a0)

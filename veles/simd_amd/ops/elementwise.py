@@ -336,3 +336,78 @@ def normalize2d(x: torch.Tensor) -> torch.Tensor:
 @normalize2d.register_fake
 def _(x):
     return torch.empty(x.shape, dtype=torch.float32, device=x.device)
+
+
+# ------------------------------------------------------------- gradients
+# Backward formulas of the differentiable elementwise ops, written with the
+# ops themselves so a GPU backward runs the same kernels.
+def _save(*idx):
+    def setup(ctx, inputs, output):
+        ctx.save_for_backward(*[inputs[i] for i in idx if isinstance(inputs[i], torch.Tensor)])
+        ctx.args = inputs
+    return setup
+
+
+def _binary_backward(ctx, g):
+    a, b, op = ctx.args
+    g = g.contiguous()
+    if op == "add":
+        return g, g, None
+    if op == "sub":
+        return g, affine(g, -1.0, 0.0), None
+    return binary(g, b, "mul"), binary(g, a, "mul"), None
+
+
+def _complex_multiply_backward(ctx, g):
+    # r = a b (or a conj(b)):  grad_a = g conj(b')  with b' the factor used,
+    # grad_b = g conj(a)  (conjugated once more when b entered conjugated)
+    a, b, conj_b = ctx.args
+    g = g.contiguous()
+    ga = complex_multiply(g, b, not conj_b)
+    gb = complex_multiply(g, a, True)
+    if conj_b:
+        gb = complex_conjugate(gb)
+    return ga, gb, None
+
+
+def _math_backward(ctx, g):
+    x, fn = ctx.args
+    g = g.contiguous()
+    if fn == "sin":
+        return binary(g, math(x, "cos"), "mul"), None
+    if fn == "cos":
+        return affine(binary(g, math(x, "sin"), "mul"), -1.0, 0.0), None
+    if fn == "exp":
+        return binary(g, math(x, "exp"), "mul"), None
+    if fn == "log":
+        return g / x, None
+    return g / affine(math(x, "sqrt"), 2.0, 0.0), None   # sqrt
+
+
+def _pow_backward(ctx, g):
+    x, y = ctx.args
+    r = pow(x, y)
+    gx = g * y * r / x
+    gy = g * r * math(x.expand_as(r).contiguous(), "log")
+    return gx.sum_to_size(x.shape), gy.sum_to_size(y.shape)
+
+
+def _sincos_backward(ctx, gs, gc):
+    x, = ctx.args
+    s, c = sincos(x)
+    return gs * c - gc * s
+
+
+binary.register_autograd(_binary_backward, setup_context=_save(0, 1))
+complex_multiply.register_autograd(_complex_multiply_backward, setup_context=_save(0, 1))
+complex_conjugate.register_autograd(lambda ctx, g: complex_conjugate(g.contiguous()),
+                                    setup_context=_save())
+affine.register_autograd(lambda ctx, g: (affine(g.contiguous(), ctx.args[1], 0.0), None, None),
+                         setup_context=_save())
+saxpy.register_autograd(lambda ctx, g: (None, affine(g.contiguous(), ctx.args[0], 0.0), g),
+                        setup_context=_save())
+math.register_autograd(_math_backward, setup_context=_save(0))
+pow.register_autograd(_pow_backward, setup_context=_save(0, 1))
+sincos.register_autograd(_sincos_backward, setup_context=_save(0))
+sum_all.register_autograd(lambda ctx, g: g.expand(ctx.args[0].shape),
+                          setup_context=_save())
