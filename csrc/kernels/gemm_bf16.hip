@@ -15,16 +15,19 @@
 // K-contiguous with whole tiles is read in place.  The main kernel
 // (gemm_glds_kernel) stages both images global -> LDS with
 // global_load_lds_dwordx4 into two XOR-swizzled stages and runs
-// v_mfma_f32_32x32x16_bf16 on 256 x 256 (bf16) / 256 x 128 (bf16x3) tiles,
-// or 128 x 128 tiles when the large ones cannot fill every CU.  (Earlier
+// v_mfma_f32_16x16x32_bf16 on 256 x 256 (bf16) / 256 x 128 (bf16x3) tiles,
+// or v_mfma_f32_32x32x16_bf16 on 128 x 128 tiles when the large ones cannot
+// fill every CU.  (Earlier
 // register-staged, three/four-stage ring and transposed-read variants were
 // measured slower or spilled and are in git history,
 // profiles/r1/gemm_modes_v*.log.)
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "csrc/kernels/device.h"
 #include "csrc/runtime/runtime.h"
@@ -245,7 +248,12 @@ __device__ __forceinline__ bf16x8 gfrag(const uint8_t *img, int row, int c) {
   return *reinterpret_cast<const bf16x8 *>(img + row * C::RB + swz<C>(row, c) * 16);
 }
 
-template <class C>
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// M16: v_mfma_f32_16x16x32_bf16 on 16 x 16 blocks (32-deep steps) instead of
+// v_mfma_f32_32x32x16_bf16 on 32 x 32 blocks (16-deep steps): the same
+// fragment reads and accumulator registers per wave.
+template <class C, bool M16 = false>
 __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
   extern __shared__ __attribute__((aligned(1024))) uint8_t glds_lds[];
   constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
@@ -280,6 +288,72 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     }
   };
 
+  const int nk = g.kp / C::BK;
+  const bool use_beta = g.beta != 0.f;
+  if constexpr (M16) {
+    constexpr int XM = 2 * TM, XN = 2 * TN;  // 16 x 16 blocks per wave
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int arow16 = wm * (C::BM / C::WM) + l16, brow16 = wn * (C::BN / C::WN) + l16;
+    floatx4 acc[XM][XN];
+#pragma unroll
+    for (int i = 0; i < XM; i++)
+#pragma unroll
+      for (int j = 0; j < XN; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
+#pragma unroll
+      for (int ks = 0; ks < C::BK / 32; ks++) {
+        const int c = 4 * ks + lq;
+        bf16x8 fa[NI][XM], fb[NI][XN];
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+#pragma unroll
+          for (int x = 0; x < XM; x++) fa[i][x] = gfrag<C>(img_a(cur, i), arow16 + 16 * x, c);
+#pragma unroll
+          for (int y = 0; y < XN; y++) fb[i][y] = gfrag<C>(img_b(cur, i), brow16 + 16 * y, c);
+        }
+#pragma unroll
+        for (int x = 0; x < XM; x++)
+#pragma unroll
+          for (int y = 0; y < XN; y++) {
+            if (C::TERMS == 3) {
+              acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][x], fb[0][y], acc[x][y],
+                                                                  0, 0, 0);
+              acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][x], fb[1][y], acc[x][y],
+                                                                  0, 0, 0);
+            }
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][x], fb[0][y], acc[x][y], 0,
+                                                                0, 0);
+          }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    // 16 x 16 block: lane l holds rows 4 (l / 16) + r, column l % 16
+#pragma unroll
+    for (int x = 0; x < XM; x++)
+#pragma unroll
+      for (int y = 0; y < XN; y++) {
+        const int col = n0 + brow16 + 16 * y;
+        if (col >= g.n) continue;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = m0 + arow16 - l16 + 16 * x + 4 * lq + r;
+          if (row < g.m) {
+            float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+            float v = g.alpha * acc[x][y][r];
+            if (use_beta) v += g.beta * *pc;
+            *pc = v;
+          }
+        }
+      }
+    return;
+  }
+
   floatx16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; i++)
@@ -288,7 +362,6 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
 #pragma unroll
       for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
 
-  const int nk = g.kp / C::BK;
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -324,7 +397,6 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     __syncthreads();
   }
 
-  const bool use_beta = g.beta != 0.f;
 #pragma unroll
   for (int x = 0; x < TM; x++)
 #pragma unroll
@@ -344,15 +416,15 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     }
 }
 
-template <class C>
+template <class C, bool M16 = false>
 vs_status launch_glds(const Args &g, int batch, hipStream_t s) {
   static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(&gemm_glds_kernel<C>),
+      reinterpret_cast<const void *>(&gemm_glds_kernel<C, M16>),
       hipFuncAttributeMaxDynamicSharedMemorySize, C::kLdsBytes);  // once per instantiation
   VS_HIP(attr);
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
-  hipLaunchKernelGGL((gemm_glds_kernel<C>), dim3(tiles, 1, static_cast<unsigned>(batch)),
+  hipLaunchKernelGGL((gemm_glds_kernel<C, M16>), dim3(tiles, 1, static_cast<unsigned>(batch)),
                      dim3(C::kThreads), C::kLdsBytes, s, g);
   VS_HIP(hipGetLastError());
   return VS_OK;
@@ -394,9 +466,13 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
     // large tiles once they fill every CU, else 128 x 128
     const long tl = static_cast<long>((m + G1::BM - 1) / G1::BM) * ((n + G1::BN - 1) / G1::BN) *
                     batch;
-    variant = tl >= 256 ? 1 : 0;
+    variant = tl >= 256 ? 2 : 0;  // the large tiles run 6 % faster on the 16 x 16 x 32 shape
   }
-  VS_REQUIRE(variant == 0 || variant == 1, "gemm_bf16: unknown variant %d (0, 1)", variant);
+  VS_REQUIRE(variant >= 0 && variant <= 3, "gemm_bf16: unknown variant %d (0..3)", variant);
+  // 0 / 1: small / large tiles on v_mfma_f32_32x32x16_bf16; 2 / 3: large / small tiles on
+  // v_mfma_f32_16x16x32_bf16
+  const bool m16 = variant >= 2;
+  variant = variant == 2 ? 1 : variant == 3 ? 0 : variant;
   const int bm = variant == 1 ? (split ? G3::BM : G1::BM) : (split ? G3S::BM : G1S::BM);
   const int bn = variant == 1 ? (split ? G3::BN : G1::BN) : (split ? G3S::BN : G1S::BN);
   const int bk = variant == 1 ? (split ? G3::BK : G1::BK) : (split ? G3S::BK : G1S::BK);
@@ -458,6 +534,9 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   g.c = c;
   g.ldc = ldc;
   g.sc = sc;
+  if (m16 && variant == 1)
+    return split ? launch_glds<G3, true>(g, batch, s) : launch_glds<G1, true>(g, batch, s);
+  if (m16) return split ? launch_glds<G3S, true>(g, batch, s) : launch_glds<G1S, true>(g, batch, s);
   if (variant == 1) return split ? launch_glds<G3>(g, batch, s) : launch_glds<G1>(g, batch, s);
   return split ? launch_glds<G3S>(g, batch, s) : launch_glds<G1S>(g, batch, s);
 }

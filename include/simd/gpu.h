@@ -189,13 +189,16 @@ vs_status vs_sgemm_variant_batched(int variant, int trans_a, int trans_b, int m,
                                    int batch, vs_stream_t stream);
 
 /// bf16 matrix-core GEMM: C (fp32) = alpha op(A) op(B) + beta C with A, B
-/// bf16 (raw uint16 bit patterns), fp32 accumulation (v_mfma_f32_32x32x16_bf16).
+/// bf16 (raw uint16 bit patterns), fp32 accumulation (v_mfma_f32_16x16x32_bf16
+/// on the large tiles, v_mfma_f32_32x32x16_bf16 on the 128 x 128 tiles).
 vs_status vs_gemm_bf16(int trans_a, int trans_b, int m, int n, int k,
                        float alpha, const uint16_t *a, int64_t lda,
                        const uint16_t *b, int64_t ldb, float beta, float *c,
                        int64_t ldc, vs_stream_t stream);
 /// Tuning entry point: explicit bf16 kernel variant (LDS-DMA two-stage;
-/// 0: 128x128 tiles, 1: 256x256 (bf16) / 256x128 (bf16x3); -1 auto).
+/// 0: 128x128 tiles, 1: 256x256 (bf16) / 256x128 (bf16x3), both on 32x32x16 MFMAs;
+/// 2 / 3: the large / small tiles on 16x16x32 MFMAs; -1 auto: 2 once the large tiles
+/// fill every CU, else 0).
 vs_status vs_gemm_bf16_variant(int variant, int trans_a, int trans_b, int m, int n,
                                int k, float alpha, const uint16_t *a, int64_t lda,
                                const uint16_t *b, int64_t ldb, float beta, float *c,
@@ -209,8 +212,7 @@ vs_status vs_gemm_bf16_strided_batched(int trans_a, int trans_b, int m, int n,
                                        int batch, vs_stream_t stream);
 /// Fast fp32 GEMM ("bf16x3"): fp32 operands split into bf16 hi + lo,
 /// C = hi hi + hi lo + lo hi on the bf16 matrix cores (~2^-16 relative
-/// error per product instead of 2^-24).  variant -1 = auto (0: 128x128,
-/// 1: 256x128 tiles).
+/// error per product instead of 2^-24).  variant as for vs_gemm_bf16_variant.
 vs_status vs_sgemm_bf16x3(int trans_a, int trans_b, int m, int n, int k,
                           float alpha, const float *a, int64_t lda,
                           const float *b, int64_t ldb, float beta, float *c,

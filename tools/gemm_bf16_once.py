@@ -22,5 +22,8 @@ s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 for _ in range(int(os.environ.get("REPS", "5"))):
     _lib.check(lib.vs_gemm_bf16_variant(v, 0, tb, n, n, n, 1.0, a.data_ptr(), n, b.data_ptr(),
                                         n, 0.0, c.data_ptr(), n, s), "bf16")
+if os.environ.get("TORCH") == "1":   # hipBLASLt on the same operands, for the counters
+    for _ in range(3):
+        torch.matmul(a, b.T if tb else b)
 torch.cuda.synchronize()
 print("ok")
