@@ -158,6 +158,7 @@ struct Args {
   float alpha, beta;
   float *c;
   int64_t ldc, sc;
+  int stagger;           // the two waves of a SIMD issue their DMA half a tile apart
 };
 
 // Pack one operand.  rows x cols is the logical op(X) with rows along the
@@ -302,9 +303,14 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // The two waves of a SIMD (wave i and i + 4) issue their share of the next
+    // tile's DMA at different times -- waves 0-3 before the tile's MFMAs, waves
+    // 4-7 a quarter of the tile later -- so one of them runs MFMAs
+    // while the other pays the DMA issue cost (60-185 cycles per piece).
+    const bool late = g.stagger && wid >= C::kWaves / 2;
     for (int kt = 0; kt < nk; kt++) {
       const int cur = kt & 1;
-      if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
+      if (!late && kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
 #pragma unroll
       for (int ks = 0; ks < C::BK / 32; ks++) {
         const int c = 4 * ks + lq;
@@ -317,7 +323,9 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
           for (int y = 0; y < XN; y++) fb[i][y] = gfrag<C>(img_b(cur, i), brow16 + 16 * y, c);
         }
 #pragma unroll
-        for (int x = 0; x < XM; x++)
+        for (int x = 0; x < XM; x++) {
+          // a quarter of the tile's MFMAs in: the late waves' DMA
+          if (ks == 0 && x == XM / 2 && late && kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
 #pragma unroll
           for (int y = 0; y < XN; y++) {
             if (C::TERMS == 3) {
@@ -329,6 +337,7 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
             acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][x], fb[0][y], acc[x][y], 0,
                                                                 0, 0);
           }
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -468,7 +477,12 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
                     batch;
     variant = tl >= 256 ? 2 : 0;  // the large tiles run 6 % faster on the 16 x 16 x 32 shape
   }
-  VS_REQUIRE(variant >= 0 && variant <= 3, "gemm_bf16: unknown variant %d (0..3)", variant);
+  VS_REQUIRE(variant >= 0 && variant <= 4, "gemm_bf16: unknown variant %d (0..4)", variant);
+  // The wave pairs of the bf16 large tile issue their DMA a quarter of a tile apart
+  // (4096^3: 1205 -> 1301 TFLOP/s, 8192^3: 1238 -> 1307; the 32-deep bf16x3 tiles lose with
+  // it: 371 -> 305); variant 4 is variant 2 without it (A/B arm).
+  const int stagger = variant == 2 && !split;
+  if (variant == 4) variant = 2;
   // 0 / 1: small / large tiles on v_mfma_f32_32x32x16_bf16; 2 / 3: large / small tiles on
   // v_mfma_f32_16x16x32_bf16
   const bool m16 = variant >= 2;
@@ -534,6 +548,7 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   g.c = c;
   g.ldc = ldc;
   g.sc = sc;
+  g.stagger = stagger;
   if (m16 && variant == 1)
     return split ? launch_glds<G3, true>(g, batch, s) : launch_glds<G1, true>(g, batch, s);
   if (m16) return split ? launch_glds<G3S, true>(g, batch, s) : launch_glds<G1S, true>(g, batch, s);

@@ -197,8 +197,9 @@ vs_status vs_gemm_bf16(int trans_a, int trans_b, int m, int n, int k,
                        int64_t ldc, vs_stream_t stream);
 /// Tuning entry point: explicit bf16 kernel variant (LDS-DMA two-stage;
 /// 0: 128x128 tiles, 1: 256x256 (bf16) / 256x128 (bf16x3), both on 32x32x16 MFMAs;
-/// 2 / 3: the large / small tiles on 16x16x32 MFMAs; -1 auto: 2 once the large tiles
-/// fill every CU, else 0).
+/// 2 / 3: the large / small tiles on 16x16x32 MFMAs (2: the two waves of a SIMD issue
+/// their DMA a quarter of a tile apart; 4: 2 without that); -1 auto: 2 once the large
+/// tiles fill every CU, else 0).
 vs_status vs_gemm_bf16_variant(int variant, int trans_a, int trans_b, int m, int n,
                                int k, float alpha, const uint16_t *a, int64_t lda,
                                const uint16_t *b, int64_t ldb, float beta, float *c,

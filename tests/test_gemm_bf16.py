@@ -111,7 +111,7 @@ def test_large_shapes_use_lds_dma_kernel(ta, tb):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_every_kernel_variant(variant):
     """Each bf16 / bf16x3 kernel variant on a ragged shape, NN and TT."""
     import ctypes
@@ -138,7 +138,7 @@ def test_every_kernel_variant(variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("ld_pad", [0, 8, 4])
 def test_whole_tile_operands_read_in_place(variant, ld_pad):
     """bf16 operands stored K-contiguous with whole tiles skip the pack
