@@ -65,8 +65,10 @@ def _child(code, **env):
     import os
     import subprocess
     import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     e = dict(os.environ, **env)
     e.pop("VELES_HOST_SMALL_SCALE", None)       # the shipped default policy
+    e["PYTHONPATH"] = repo + os.pathsep + e.get("PYTHONPATH", "")   # whatever the cwd is
     e.update(env)
     r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True,
                        timeout=300)
