@@ -342,6 +342,48 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+    // C through LDS: a 16 x 16 block leaves lane l with rows 4 (l / 16) + r of
+    // column l % 16, i.e. 64-byte row segments and one dword store per value
+    // (4096 dword stores per wave).  Each wave turns 32 rows
+    // x 64 columns at a time round through its own LDS patch (row stride 68
+    // floats: conflict-free both ways) and stores float4 per lane, 256-byte
+    // row segments.
+    const bool vec = (g.ldc & 3) == 0 && (g.sc & 3) == 0 &&
+                     (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
+    if (vec) {
+      constexpr int LDW = 68, WN64 = C::BN / C::WN;  // patch row stride (floats); wave tile width
+      static_assert(WN64 == 64, "the patch is 64 columns wide");
+      float *patch = reinterpret_cast<float *>(glds_lds) + wid * 32 * LDW;
+      const int wrow0 = m0 + wm * (C::BM / C::WM), wcol0 = n0 + wn * WN64;
+#pragma unroll
+      for (int p = 0; p < XM / 2; p++) {
+#pragma unroll
+        for (int xx = 0; xx < 2; xx++)
+#pragma unroll
+          for (int y = 0; y < XN; y++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+              patch[(16 * xx + 4 * lq + r) * LDW + 16 * y + l16] = g.alpha * acc[2 * p + xx][y][r];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const int pr = 4 * i + lq, pc4 = 4 * l16;
+          const floatx4 v = *reinterpret_cast<const floatx4 *>(patch + pr * LDW + pc4);
+          const int row = wrow0 + 32 * p + pr, col = wcol0 + pc4;
+          if (row >= g.m || col >= g.n) continue;
+          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+          if (col + 3 < g.n) {
+            floatx4 o = v;
+            if (use_beta) o += g.beta * *reinterpret_cast<const floatx4 *>(pc);
+            *reinterpret_cast<floatx4 *>(pc) = o;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+              if (col + e < g.n) pc[e] = use_beta ? v[e] + g.beta * pc[e] : v[e];
+          }
+        }
+      }
+      return;
+    }
     // 16 x 16 block: lane l holds rows 4 (l / 16) + r, column l % 16
 #pragma unroll
     for (int x = 0; x < XM; x++)
