@@ -1143,7 +1143,8 @@ thread_local int g_conv_real = 1;
 thread_local int g_conv_real_all = 0;
 
 bool use_real(int logl);
-int fdl_part_taps();
+int fdl_block_log(int hlen);
+int fdl_part_taps(int hlen);
 constexpr int kFdlMaxParts = 20;
 
 // Longest row one kernel launch sequence handles: the buffer-descriptor
@@ -1211,8 +1212,11 @@ int select(int64_t xlen, int hlen, int batch) {
   // run 66, the fused four-step transform 70 whatever the filter), else one
   // padded transform
   // while it exists (vs_conv1d never fails for a valid shape).
-  const int parts = (hlen + fdl_part_taps() - 1) / fdl_part_taps();
-  return parts <= kFdlMaxParts || lm > fft::kMaxLog ? VS_CONV_OVERLAP_SAVE : VS_CONV_FFT;
+  const int parts = (hlen + fdl_part_taps(hlen) - 1) / fdl_part_taps(hlen);
+  // L = 32768 blocks (filters past 20 partitions of 8192 taps): 13 partitions run 72
+  // Gsamples/s, 25 run 55
+  const int max_parts = fdl_block_log(hlen) == 15 ? 14 : kFdlMaxParts;
+  return parts <= max_parts || lm > fft::kMaxLog ? VS_CONV_OVERLAP_SAVE : VS_CONV_FFT;
 }
 
 // Every run_* entry writes the first `ylen` outputs (<= xlen + hlen - 1) of
@@ -1380,7 +1384,7 @@ vs_status run_real(int correlate, bool overlap_save, const float *x, int xlen, i
 }
 
 // Filters too long for one overlap-save block: uniformly partitioned
-// overlap-save (fdl_*_kernel above).  Blocks of L = 2^g_fdl_log samples, B =
+// overlap-save (fdl_*_kernel above).  Blocks of L = 2^fdl_block_log(hlen) samples, B =
 // L / 2 taps per partition.  `pq_pre`: the partitions' P / Q tables when a
 // plan holds them.  Signals go through in groups whose spectra (Z and Y:
 // 16 bytes per sample and per output) fit kFdlScratch.
@@ -1470,17 +1474,29 @@ vs_status run_fdl_t(int correlate, const float *x, int xlen, int64_t xs, const f
   return VS_OK;
 }
 
-// log2 of the block of the partitioned path (vs_tune_set("fdl_block_log")).
-thread_local int g_fdl_log = 14;
+// log2 of the block of the partitioned path: vs_tune_set("fdl_block_log") 13 / 14 / 15, or
+// 0 = by filter length: L = 16384 up to 20 partitions of 8192 taps, L = 32768 beyond (the
+// larger transforms run slower per sample -- one workgroup per CU -- but halve the spectral
+// accumulation: per-signal filters of 65,536 / 200,000 / 400,000 taps at 2^20 x 64 run
+// 95 / 59 / 35 Gsamples/s on L = 16384 and 86 / 65 / 46 on L = 32768,
+// profiles/r3/conv/fdl.md).
+thread_local int g_fdl_log = 0;
 
-int fdl_part_taps() { return 1 << (g_fdl_log - 1); }
+int fdl_block_log(int hlen) {
+  if (g_fdl_log) return g_fdl_log;
+  return hlen > kFdlMaxParts * 8192 ? 15 : 14;
+}
+int fdl_part_taps(int hlen) { return 1 << (fdl_block_log(hlen) - 1); }
 
 vs_status run_partitioned(int correlate, const float *x, int xlen, int64_t xs,
                           const float *h, int hlen, int64_t hs, float *y, int64_t ys, int ylen,
                           int batch, hipStream_t s, const float4 *pq_pre = nullptr,
                           int logl = 0) {
-  if ((logl ? logl : g_fdl_log) == 13)
+  const int l = logl ? logl : fdl_block_log(hlen);
+  if (l == 13)
     return run_fdl_t<12, 0>(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s, pq_pre);
+  if (l == 15)
+    return run_fdl_t<14, 0>(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s, pq_pre);
   return run_fdl_t<13, 32>(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s, pq_pre);
 }
 
@@ -1591,7 +1607,7 @@ vs_status vs_conv1d_plan_create(int algo, int correlate, int64_t xlen, const flo
     if (conv::os_single_block(hlen)) {
       if (conv::use_real(l)) logl = l, os = true;
     } else {  // partitioned: one P / Q table per partition
-      logl = conv::g_fdl_log == 13 ? 13 : 14;
+      logl = conv::fdl_block_log(hlen);
       parts = (hlen + (1 << (logl - 1)) - 1) >> (logl - 1);
       os = true;
     }
@@ -1743,7 +1759,7 @@ vs_status vs_tune_set(const char *key, int value) {
     return VS_OK;
   }
   if (std::strcmp(key, "fdl_block_log") == 0) {
-    VS_REQUIRE(value == 13 || value == 14, "fdl_block_log must be 13 or 14");
+    VS_REQUIRE(value == 0 || (value >= 13 && value <= 15), "fdl_block_log must be 0 (by filter length), 13, 14 or 15");
     conv::g_fdl_log = value;
     return VS_OK;
   }
@@ -1769,7 +1785,7 @@ void vs_tune_reset(void) {
   conv::g_conv_buf = 1;
   conv::g_conv_real = 1;
   conv::g_conv_real_all = 0;
-  conv::g_fdl_log = 14;
+  conv::g_fdl_log = 0;
   conv::g_fdl_mac_lds = 1;
   conv::g_fdl_mac_chunk = 0;
   conv::g_piece_log = 28;
@@ -1801,7 +1817,7 @@ vs_status dispatch(int algo, int correlate, const float *x, int xlen, int64_t xs
         return run_block(correlate, true, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s);
       }
       log(1, "vs_conv1d: filter %d longer than an overlap-save block: %d partitions", hlen,
-          (hlen + fdl_part_taps() - 1) / fdl_part_taps());
+          (hlen + fdl_part_taps(hlen) - 1) / fdl_part_taps(hlen));
       return run_partitioned(correlate, x, xlen, xs, h, hlen, hs, y, ys, ylen, batch, s);
     case VS_CONV_FFT:
       if (lm <= fft::kMaxLdsLog || (lm == fft::kMaxLdsLog + 1 && use_real(lm))) {

@@ -189,7 +189,7 @@ def test_partitioned_beyond_32768_block():
     _check(200000, 40000, 1, "overlap_save", True)
 
 
-@pytest.mark.parametrize("block_log", [14, 13])
+@pytest.mark.parametrize("block_log", [14, 13, 15])
 @pytest.mark.parametrize("xlen,hlen,batch,per_signal", [
     (1 << 18, 65536, 2, False),    # 8 partitions of 8192 taps
     (100003, 200000, 2, False),    # filter longer than the signal, ragged last partition
@@ -202,7 +202,7 @@ def test_uniformly_partitioned_overlap_save(block_log, xlen, hlen, batch, per_si
     """Frequency-domain delay line (conv.hip fdl_*_kernel): every x block
     transformed once, partition spectra accumulated per output block, one
     inverse per block; both block sizes (L = 16384 default, 8192)."""
-    with _knob("fdl_block_log", block_log, 14):
+    with _knob("fdl_block_log", block_log, 0):
         _check(xlen, hlen, batch, "overlap_save", corr, per_signal=per_signal)
 
 
@@ -213,7 +213,7 @@ def test_partitioned_many_output_tiles(lds):
     (tile, partition group) edge of both accumulation kernels."""
     with _knob("fdl_mac_lds", lds, 1):
         _check(8192 * 37 + 5, 8192 * 5 + 77, 2, "overlap_save", False)
-        with _knob("fdl_block_log", 13, 14):
+        with _knob("fdl_block_log", 13, 0):
             _check(4096 * 41 + 3, 4096 * 9 + 1, 1, "overlap_save", True)
             _check(4096 * 70 + 3, 4096 * 2 + 1, 2, "overlap_save", False, per_signal=True)
 
@@ -221,7 +221,7 @@ def test_partitioned_many_output_tiles(lds):
 def test_partitioned_more_partitions_than_one_lds_chunk():
     """40 and 67 partitions of 4096 taps: the LDS-staged accumulation walks them
     in chunks of 32 (two and three chunks), against the register kernel."""
-    with _knob("fdl_block_log", 13, 14):
+    with _knob("fdl_block_log", 13, 0):
         for hlen in (4096 * 39 + 11, 4096 * 66 + 4095):
             _check(4096 * 45 + 9, hlen, 2, "overlap_save", False)
             with _knob("fdl_mac_lds", 0, 1):
@@ -312,7 +312,8 @@ def test_select_long_filter_overlap_save():
     """Filters whose L = 32768 block is >= 28 % useful run single-block
     overlap-save (h = 20000: 144 vs 73 Gsamples/s for the fused four-step
     FFT); longer ones the uniformly partitioned path up to 20 partitions of
-    8192 taps (h = 65536: 100 vs 70, h = 163840: 73 vs 70), then the FFT
+    8192 taps (h = 65536: 100 vs 70, h = 163840: 73 vs 70), then up to 14
+    partitions of 16384 taps (h = 200000: 72 vs 70), then the FFT
     (profiles/r3/conv/fdl.md)."""
     from veles.simd_amd import _lib
     lib = _lib.lib()
@@ -320,8 +321,10 @@ def test_select_long_filter_overlap_save():
     assert lib.vs_conv1d_select(1 << 20, 30000, 64) == 3
     assert lib.vs_conv1d_select(1 << 20, 98304, 64) == 3
     assert lib.vs_conv1d_select(1 << 20, 163840, 64) == 3
-    assert lib.vs_conv1d_select(1 << 20, 163841, 64) == 2
-    assert lib.vs_conv1d_select(1 << 20, 200000, 64) == 2
+    assert lib.vs_conv1d_select(1 << 20, 200000, 64) == 3    # 13 partitions of 16384 taps
+    assert lib.vs_conv1d_select(1 << 20, 229376, 64) == 3    # 14
+    assert lib.vs_conv1d_select(1 << 20, 229377, 64) == 2
+    assert lib.vs_conv1d_select(1 << 20, 400000, 64) == 2
     assert lib.vs_conv1d_select(1 << 27, 200000, 1) == 3   # beyond the largest transform
     _check(200000, 20000, 2, "auto", False)
     _check(200000, 20000, 1, "auto", True)
