@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the GEMM modes at square sizes (median of interleaved rounds):
-exact fp32 MFMA (vs_sgemm), bf16x3 fast fp32 (variants 0/1), bf16 matrix
-cores, and torch.matmul fp32 / bf16 (hipBLASLt) for context.  TFLOP/s are
+exact fp32 MFMA (vs_sgemm), bf16x3 fast fp32, bf16 matrix cores (NN through the
+pack prepass, NT read in place; kernel variants: tools/bench_gemm_bf16.py), and torch.matmul fp32 / bf16 (hipBLASLt) for context.  TFLOP/s are
 2 n^3 / t for every mode (the bf16x3 figure is fp32-equivalent throughput)."""
 import ctypes
 import json
@@ -32,29 +32,14 @@ def main():
         modes = {
             "exact": lambda: lib.vs_sgemm(0, 0, n, n, n, 1.0, a.data_ptr(), n, b.data_ptr(), n,
                                           0.0, c.data_ptr(), n, s),
-            "bf16x3_v2": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
-                                                     b.data_ptr(), n, 0.0, c.data_ptr(), n, 2, s),
-            "bf16x3_v3": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
-                                                     b.data_ptr(), n, 0.0, c.data_ptr(), n, 3, s),
+            "bf16x3": lambda: lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, a.data_ptr(), n,
+                                                  b.data_ptr(), n, 0.0, c.data_ptr(), n, -1, s),
             "bf16": lambda: lib.vs_gemm_bf16_strided_batched(0, 0, n, n, n, 1.0, ah.data_ptr(),
                                                              n, 0, bh.data_ptr(), n, 0, 0.0,
                                                              c.data_ptr(), n, 0, 1, s),
-            "bf16_v2": lambda: lib.vs_gemm_bf16_variant(2, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
-                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
-            "bf16_v3": lambda: lib.vs_gemm_bf16_variant(3, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
-                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
-            "bf16_v4": lambda: lib.vs_gemm_bf16_variant(4, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
-                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
-            "bf16_v6": lambda: lib.vs_gemm_bf16_variant(6, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
-                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
-            "bf16_v5": lambda: lib.vs_gemm_bf16_variant(5, 0, 0, n, n, n, 1.0, ah.data_ptr(), n,
-                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n, s),
-            "bf16_nt_v2": lambda: lib.vs_gemm_bf16_variant(2, 0, 1, n, n, n, 1.0, ah.data_ptr(), n,
-                                                           bh.data_ptr(), n, 0.0, c.data_ptr(), n,
-                                                           s),
-            "bf16_nt_v5": lambda: lib.vs_gemm_bf16_variant(5, 0, 1, n, n, n, 1.0, ah.data_ptr(), n,
-                                                           bh.data_ptr(), n, 0.0, c.data_ptr(), n,
-                                                           s),
+            "bf16_nt": lambda: lib.vs_gemm_bf16_variant(-1, 0, 1, n, n, n, 1.0, ah.data_ptr(), n,
+                                                        bh.data_ptr(), n, 0.0, c.data_ptr(), n,
+                                                        s),
             "torch_fp32": lambda: torch.matmul(a, b, out=c),
             "torch_bf16": lambda: torch.matmul(ah, bh),
         }
