@@ -1,9 +1,9 @@
-// Host paths for calls too small to be worth a GPU round trip (about 11 us of
-// launch + wait on MI355X): direct convolution / correlation and single
-// wavelet levels on a few hundred samples.  The scalar functions of ref.cpp
-// stay the semantic reference (simd = 0, `_na`); these compute the same sums
-// with unit-stride inner loops the host compiler vectorises, built for the
-// baseline ISA and for AVX2 + FMA with load-time dispatch (target_clones).
+// Host paths for calls too small to be worth a GPU round trip (14-18 us on
+// MI355X): direct convolution / correlation, single wavelet levels, small
+// matrix sums and products.  The scalar functions of ref.cpp stay the
+// semantic reference (simd = 0, `_na`); these compute the same sums with
+// unit-stride inner loops the host compiler vectorises, built for the
+// baseline ISA and for AVX2 + FMA and chosen at run time by CPU feature.
 // The reference's counterparts are its hand-written AVX loops
 // (reference src/convolve.c:49-100, src/wavelet.c:395-1555).
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
