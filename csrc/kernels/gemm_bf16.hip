@@ -260,10 +260,16 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
   constexpr int TM = C::TM, TN = C::TN, NI = C::NIMG;
   const unsigned tiles_m = (g.m + C::BM - 1) / C::BM;
   const unsigned tiles_n = (g.n + C::BN - 1) / C::BN;
-  const unsigned t = dev::xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  unsigned tm, tn;
-  dev::grouped_tile(t, tiles_m, tiles_n, tm, tn);
-  const int m0 = static_cast<int>(tm) * C::BM, n0 = static_cast<int>(tn) * C::BN;
+  const unsigned ntiles = tiles_m * tiles_n;
+  unsigned tile = blockIdx.x;  // the M16 form walks tiles blockIdx.x, + gridDim.x, ...
+  int m0, n0;
+  const auto place = [&] {
+    unsigned tm, tn;
+    dev::grouped_tile(dev::xcd_remap(tile, ntiles), tiles_m, tiles_n, tm, tn);
+    m0 = static_cast<int>(tm) * C::BM;
+    n0 = static_cast<int>(tn) * C::BN;
+  };
+  place();
   const uint16_t *A[2], *B[2];
 #pragma unroll
   for (int i = 0; i < NI; i++) {
@@ -296,6 +302,7 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     const int l16 = lane & 15, lq = lane >> 4;
     const int arow16 = wm * (C::BM / C::WM) + l16, brow16 = wn * (C::BN / C::WN) + l16;
     floatx4 acc[XM][XN];
+    for (;;) {
 #pragma unroll
     for (int i = 0; i < XM; i++)
 #pragma unroll
@@ -382,8 +389,7 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
           }
         }
       }
-      return;
-    }
+    } else {
     // 16 x 16 block: lane l holds rows 4 (l / 16) + r, column l % 16
 #pragma unroll
     for (int x = 0; x < XM; x++)
@@ -402,7 +408,12 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
           }
         }
       }
-    return;
+    }
+    tile += gridDim.x;
+    if (tile >= ntiles) return;
+    place();
+    __syncthreads();  // the LDS patches are read before the next tile's DMA lands on them
+    }
   }
 
   floatx16 acc[TM][TN];
@@ -475,7 +486,10 @@ vs_status launch_glds(const Args &g, int batch, hipStream_t s) {
   VS_HIP(attr);
   const unsigned tiles = static_cast<unsigned>(((g.m + C::BM - 1) / C::BM) *
                                                ((g.n + C::BN - 1) / C::BN));
-  hipLaunchKernelGGL((gemm_glds_kernel<C, M16>), dim3(tiles, 1, static_cast<unsigned>(batch)),
+  // g.stagger & 2: the 16 x 16 x 32 form as one workgroup per CU walking the tiles
+  const unsigned grid = M16 && (g.stagger & 2)
+                            ? std::min(tiles, static_cast<unsigned>(device_cu_count())) : tiles;
+  hipLaunchKernelGGL((gemm_glds_kernel<C, M16>), dim3(grid, 1, static_cast<unsigned>(batch)),
                      dim3(C::kThreads), C::kLdsBytes, s, g);
   VS_HIP(hipGetLastError());
   return VS_OK;
@@ -522,8 +536,10 @@ vs_status gemm_impl(bool split, int ta, int tb, int m, int n, int k, float alpha
   VS_REQUIRE(variant >= 0 && variant <= 4, "gemm_bf16: unknown variant %d (0..4)", variant);
   // The wave pairs of the bf16 large tile issue their DMA a quarter of a tile apart
   // (4096^3: 1205 -> 1301 TFLOP/s, 8192^3: 1238 -> 1307; the 32-deep bf16x3 tiles lose with
-  // it: 371 -> 305); variant 4 is variant 2 without it (A/B arm).
-  const int stagger = variant == 2 && !split;
+  // it: 371 -> 305); variant 4 is variant 2 without it and without the tile walk (A/B arm).
+  // bit 0: staggered DMA issue; bit 1: one workgroup per CU walks the tiles (+2 % on the bf16
+  // large tile: no workgroup turnaround between tiles; the bf16x3 tiles lose with it)
+  const int stagger = variant == 2 && !split ? 3 : 0;
   if (variant == 4) variant = 2;
   // 0 / 1: small / large tiles on v_mfma_f32_32x32x16_bf16; 2 / 3: large / small tiles on
   // v_mfma_f32_16x16x32_bf16
