@@ -159,7 +159,7 @@ def main():
 
     # Fast-fp32 mode on the bf16 matrix cores (hi/lo split, 3 products;
     # ~2^-17 relative per product): reported for context, NOT the headline.
-    if hasattr(lib, "vs_sgemm_bf16x3"):
+    def _x3_section():
         def x3_step():
             st = lib.vs_sgemm_bf16x3(0, 0, n, n, n, 1.0, pa, n, pb, n, 0.0, pc, n, -1, stream)
             if st:
@@ -170,7 +170,6 @@ def main():
             2.0 * n ** 3 * max(5, args.steps // 2) * world / dt3 / 1e9, 1)
         secondary["sgemm_bf16x3_max_abs_err"] = err3
 
-    # ----------------------------------------------------------------- conv
     # A failure in a secondary section (it would be the same on every rank: a
     # shape or API error, not a lost rank) is recorded instead of losing the
     # headline line.
@@ -180,6 +179,32 @@ def main():
         except Exception as e:  # noqa: BLE001
             secondary[name + "_error"] = f"{type(e).__name__}: {e}"[:300]
 
+    # bf16 matrix-core GEMM (fp32 accumulate and fp32 C), NT form (both operands
+    # K-contiguous, read in place), for context: NOT the headline.
+    def _bf16_section():
+        ah = a.bfloat16()
+        bth = b.t().contiguous().bfloat16()    # [n][k]
+        pah, pbh = ctypes.c_void_p(ah.data_ptr()), ctypes.c_void_p(bth.data_ptr())
+
+        def bf16_step():
+            st = lib.vs_gemm_bf16_variant(-1, 0, 1, n, n, n, 1.0, pah, n, pbh, n, 0.0, pc, n,
+                                          stream)
+            if st:
+                raise RuntimeError(lib.vs_last_error().decode())
+        bsteps = max(20, args.steps)
+        dtb = _timed(bf16_step, bsteps, 3, dist_on)
+        errb = (c[:256].double() - ah[:256].double() @ bth.double().t()).abs().max().item()
+        dtbt = _timed(lambda: torch.matmul(ah, bth.t()), bsteps, 3, dist_on)
+        secondary["gemm_bf16_gflops"] = round(2.0 * n ** 3 * bsteps * world / dtb / 1e9, 1)
+        secondary["gemm_bf16_max_abs_err"] = errb
+        secondary["torch_matmul_bf16_gflops"] = round(2.0 * n ** 3 * bsteps * world / dtbt / 1e9, 1)
+
+    if hasattr(lib, "vs_sgemm_bf16x3"):
+        _secondary("sgemm_bf16x3", _x3_section)
+    if hasattr(lib, "vs_gemm_bf16_variant"):
+        _secondary("gemm_bf16", _bf16_section)
+
+    # ----------------------------------------------------------------- conv
     def _conv_section():
         x = torch.randn((CONV_BATCH, CONV_LEN), device="cuda", generator=g)
         h = torch.randn((CONV_H,), device="cuda", generator=g)
