@@ -239,8 +239,8 @@ __device__ __forceinline__ void dma_image(const uint16_t *__restrict__ img, int6
     const int pc = lane % C::NC;                // physical chunk it fills
     const int c = swz<C>(row, pc);              // logical chunk stored there
     const uint16_t *src = img + static_cast<int64_t>(row0 + row) * ld + k0 + 8 * c;
-    __builtin_amdgcn_global_load_lds((glob_void *)const_cast<uint16_t *>(src), (lds_void *)(dst + j * 1024), 16, 0,
-                                     0);
+    __builtin_amdgcn_global_load_lds((glob_void *)const_cast<uint16_t *>(src),
+                                     (lds_void *)(dst + j * 1024), 16, 0, 0);
   }
 }
 
@@ -304,115 +304,116 @@ __global__ __launch_bounds__(C::kThreads) void gemm_glds_kernel(Args g) {
     floatx4 acc[XM][XN];
     for (;;) {
 #pragma unroll
-    for (int i = 0; i < XM; i++)
+      for (int i = 0; i < XM; i++)
 #pragma unroll
-      for (int j = 0; j < XN; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // The two waves of a SIMD (wave i and i + 4) issue their share of the next
-    // tile's DMA at different times -- waves 0-3 before the tile's MFMAs, waves
-    // 4-7 a quarter of the tile later -- so one of them runs MFMAs
-    // while the other pays the DMA issue cost (60-185 cycles per piece).
-    const bool late = g.stagger && wid >= C::kWaves / 2;
-    for (int kt = 0; kt < nk; kt++) {
-      const int cur = kt & 1;
-      if (!late && kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
-#pragma unroll
-      for (int ks = 0; ks < C::BK / 32; ks++) {
-        const int c = 4 * ks + lq;
-        bf16x8 fa[NI][XM], fb[NI][XN];
-#pragma unroll
-        for (int i = 0; i < NI; i++) {
-#pragma unroll
-          for (int x = 0; x < XM; x++) fa[i][x] = gfrag<C>(img_a(cur, i), arow16 + 16 * x, c);
-#pragma unroll
-          for (int y = 0; y < XN; y++) fb[i][y] = gfrag<C>(img_b(cur, i), brow16 + 16 * y, c);
-        }
-#pragma unroll
-        for (int x = 0; x < XM; x++) {
-          // a quarter of the tile's MFMAs in: the late waves' DMA
-          if (ks == 0 && x == XM / 2 && late && kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
-#pragma unroll
-          for (int y = 0; y < XN; y++) {
-            if (C::TERMS == 3) {
-              acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][x], fb[0][y], acc[x][y],
-                                                                  0, 0, 0);
-              acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][x], fb[1][y], acc[x][y],
-                                                                  0, 0, 0);
-            }
-            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][x], fb[0][y], acc[x][y], 0,
-                                                                0, 0);
-          }
-        }
-      }
+        for (int j = 0; j < XN; j++) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      stage(0, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-    }
-    // C through LDS: a 16 x 16 block leaves lane l with rows 4 (l / 16) + r of
-    // column l % 16, i.e. 64-byte row segments and one dword store per value
-    // (4096 dword stores per wave).  Each wave turns 32 rows
-    // x 64 columns at a time round through its own LDS patch (row stride 68
-    // floats: conflict-free both ways) and stores float4 per lane, 256-byte
-    // row segments.
-    const bool vec = (g.ldc & 3) == 0 && (g.sc & 3) == 0 &&
-                     (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
-    if (vec) {
-      constexpr int LDW = 68, WN64 = C::BN / C::WN;  // patch row stride (floats); wave tile width
-      static_assert(WN64 == 64, "the patch is 64 columns wide");
-      float *patch = reinterpret_cast<float *>(glds_lds) + wid * 32 * LDW;
-      const int wrow0 = m0 + wm * (C::BM / C::WM), wcol0 = n0 + wn * WN64;
+      // The two waves of a SIMD (wave i and i + 4) issue their share of the next
+      // tile's DMA at different times -- waves 0-3 before the tile's MFMAs, waves
+      // 4-7 a quarter of the tile later -- so one of them runs MFMAs
+      // while the other pays the DMA issue cost (60-185 cycles per piece).
+      const bool late = g.stagger && wid >= C::kWaves / 2;
+      for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        if (!late && kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
 #pragma unroll
-      for (int p = 0; p < XM / 2; p++) {
+        for (int ks = 0; ks < C::BK / 32; ks++) {
+          const int c = 4 * ks + lq;
+          bf16x8 fa[NI][XM], fb[NI][XN];
 #pragma unroll
-        for (int xx = 0; xx < 2; xx++)
+          for (int i = 0; i < NI; i++) {
 #pragma unroll
-          for (int y = 0; y < XN; y++)
+            for (int x = 0; x < XM; x++) fa[i][x] = gfrag<C>(img_a(cur, i), arow16 + 16 * x, c);
 #pragma unroll
-            for (int r = 0; r < 4; r++)
-              patch[(16 * xx + 4 * lq + r) * LDW + 16 * y + l16] = g.alpha * acc[2 * p + xx][y][r];
+            for (int y = 0; y < XN; y++) fb[i][y] = gfrag<C>(img_b(cur, i), brow16 + 16 * y, c);
+          }
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const int pr = 4 * i + lq, pc4 = 4 * l16;
-          const floatx4 v = *reinterpret_cast<const floatx4 *>(patch + pr * LDW + pc4);
-          const int row = wrow0 + 32 * p + pr, col = wcol0 + pc4;
-          if (row >= g.m || col >= g.n) continue;
-          float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
-          if (col + 3 < g.n) {
-            floatx4 o = v;
-            if (use_beta) o += g.beta * *reinterpret_cast<const floatx4 *>(pc);
-            *reinterpret_cast<floatx4 *>(pc) = o;
-          } else {
+          for (int x = 0; x < XM; x++) {
+            // a quarter of the tile's MFMAs in: the late waves' DMA
+            if (ks == 0 && x == XM / 2 && late && kt + 1 < nk) stage(cur ^ 1, (kt + 1) * C::BK);
 #pragma unroll
-            for (int e = 0; e < 4; e++)
-              if (col + e < g.n) pc[e] = use_beta ? v[e] + g.beta * pc[e] : v[e];
+            for (int y = 0; y < XN; y++) {
+              if (C::TERMS == 3) {
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][x], fb[0][y], acc[x][y],
+                                                                    0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][x], fb[1][y], acc[x][y],
+                                                                    0, 0, 0);
+              }
+              acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][x], fb[0][y], acc[x][y], 0,
+                                                                  0, 0);
+            }
           }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
-    } else {
-    // 16 x 16 block: lane l holds rows 4 (l / 16) + r, column l % 16
+      // C through LDS: a 16 x 16 block leaves lane l with rows 4 (l / 16) + r of
+      // column l % 16, i.e. 64-byte row segments and one dword store per value
+      // (4096 dword stores per wave).  Each wave turns 32 rows
+      // x 64 columns at a time round through its own LDS patch (row stride 68
+      // floats: conflict-free both ways) and stores float4 per lane, 256-byte
+      // row segments.
+      const bool vec = (g.ldc & 3) == 0 && (g.sc & 3) == 0 &&
+                       (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
+      if (vec) {
+        constexpr int LDW = 68, WN64 = C::BN / C::WN;  // patch row stride (floats); wave tile width
+        static_assert(WN64 == 64, "the patch is 64 columns wide");
+        float *patch = reinterpret_cast<float *>(glds_lds) + wid * 32 * LDW;
+        const int wrow0 = m0 + wm * (C::BM / C::WM), wcol0 = n0 + wn * WN64;
 #pragma unroll
-    for (int x = 0; x < XM; x++)
+        for (int p = 0; p < XM / 2; p++) {
 #pragma unroll
-      for (int y = 0; y < XN; y++) {
-        const int col = n0 + brow16 + 16 * y;
-        if (col >= g.n) continue;
+          for (int xx = 0; xx < 2; xx++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = m0 + arow16 - l16 + 16 * x + 4 * lq + r;
-          if (row < g.m) {
+            for (int y = 0; y < XN; y++)
+#pragma unroll
+              for (int r = 0; r < 4; r++)
+                patch[(16 * xx + 4 * lq + r) * LDW + 16 * y + l16] =
+                    g.alpha * acc[2 * p + xx][y][r];
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const int pr = 4 * i + lq, pc4 = 4 * l16;
+            const floatx4 v = *reinterpret_cast<const floatx4 *>(patch + pr * LDW + pc4);
+            const int row = wrow0 + 32 * p + pr, col = wcol0 + pc4;
+            if (row >= g.m || col >= g.n) continue;
             float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
-            float v = g.alpha * acc[x][y][r];
-            if (use_beta) v += g.beta * *pc;
-            *pc = v;
+            if (col + 3 < g.n) {
+              floatx4 o = v;
+              if (use_beta) o += g.beta * *reinterpret_cast<const floatx4 *>(pc);
+              *reinterpret_cast<floatx4 *>(pc) = o;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; e++)
+                if (col + e < g.n) pc[e] = use_beta ? v[e] + g.beta * pc[e] : v[e];
+            }
           }
         }
+      } else {
+        // 16 x 16 block: lane l holds rows 4 (l / 16) + r, column l % 16
+#pragma unroll
+        for (int x = 0; x < XM; x++)
+#pragma unroll
+          for (int y = 0; y < XN; y++) {
+            const int col = n0 + brow16 + 16 * y;
+            if (col >= g.n) continue;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              const int row = m0 + arow16 - l16 + 16 * x + 4 * lq + r;
+              if (row < g.m) {
+                float *pc = Cp + static_cast<int64_t>(row) * g.ldc + col;
+                float v = g.alpha * acc[x][y][r];
+                if (use_beta) v += g.beta * *pc;
+                *pc = v;
+              }
+            }
+          }
       }
-    }
-    tile += gridDim.x;
-    if (tile >= ntiles) return;
-    place();
-    __syncthreads();  // the LDS patches are read before the next tile's DMA lands on them
+      tile += gridDim.x;
+      if (tile >= ntiles) return;
+      place();
+      __syncthreads();  // the LDS patches are read before the next tile's DMA lands on them
     }
   }
 
