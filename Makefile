@@ -56,6 +56,9 @@ $(TEST_BIN): tests/native/capi_test.cpp $(LIB) $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -O2 -std=c++17 -Iinclude -Itests/native $< -o $@ \
 	    -L$(LIBDIR) -lvelessimd -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+	$(HIPCC) -O2 -std=c++17 -Iinclude -Itests/native tests/native/threads_test.cpp \
+	    -o $(dir $@)threads_test -L$(LIBDIR) -lvelessimd -lpthread \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 clean:
 	rm -rf $(BUILD) $(LIB)
@@ -116,6 +119,21 @@ asan:
 	    -L$(ASAN_BUILD)/lib -lvelessimd -Wl,-rpath,'$$ORIGIN/../lib'
 
 .PHONY: asan
+
+# Host ThreadSanitizer build + the multi-threaded native test (host code only).
+#   make tsan && VELES_DISABLE_GPU=1 build-tsan/tests/threads_test 8 5
+TSAN_BUILD := build-tsan
+TSAN_FLAGS := -O1 -g -fno-omit-frame-pointer
+tsan:
+	$(MAKE) BUILD=$(TSAN_BUILD) OPT="$(TSAN_FLAGS) -Xarch_host -fsanitize=thread" \
+	    LIBDIR=$(TSAN_BUILD)/lib LIB=$(TSAN_BUILD)/lib/libvelessimd.so \
+	    LDEXTRA=-fsanitize=thread TEST_BIN=$(TSAN_BUILD)/tests/capi_test lib
+	@mkdir -p $(TSAN_BUILD)/tests
+	$(HIPCC) $(TSAN_FLAGS) -Xarch_host -fsanitize=thread -std=c++17 -Iinclude -Itests/native \
+	    tests/native/threads_test.cpp -o $(TSAN_BUILD)/tests/threads_test \
+	    -L$(TSAN_BUILD)/lib -lvelessimd -lpthread -Wl,-rpath,'$$ORIGIN/../lib'
+
+.PHONY: tsan
 
 # Host line coverage (gcov), the counterpart of the reference's
 # --enable-test-coverage (common.ac:229-236): host code of every source built

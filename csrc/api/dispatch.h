@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <climits>
 #include <cstddef>
 #include <initializer_list>
@@ -37,11 +38,9 @@ inline int checked_int(const char *what, size_t n) {
 inline bool use_gpu_simd(int simd, const char *fn) {
   if (!simd) return false;
   if (gpu_available()) return true;
-  static bool warned = false;
-  if (!warned) {
-    warned = true;
+  static std::atomic<bool> warned{false};  // calls may come from several threads
+  if (!warned.exchange(true))
     log(1, "%s: no GPU visible, accelerated path runs the host reference", fn);
-  }
   return false;
 }
 

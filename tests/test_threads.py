@@ -70,3 +70,17 @@ def test_host_api_from_many_threads_host_paths():
 @pytest.mark.gpu
 def test_host_api_from_many_threads_gpu_paths():
     _run(8, 10)
+
+
+def test_native_thread_test_binary():
+    """tests/native/threads_test.cpp (the program `make tsan` runs under
+    ThreadSanitizer) built against the regular library: 8 threads x 3 rounds."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "build", "tests", "threads_test")
+    if not os.path.exists(exe):
+        pytest.skip("build/tests/threads_test not built (make tests)")
+    r = subprocess.run([exe, "8", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failure(s)" in r.stdout
