@@ -135,6 +135,19 @@ tsan:
 
 .PHONY: tsan
 
+# Host UndefinedBehaviorSanitizer build (shared runtime, so the CPU pytest suite can load
+# the library into an uninstrumented python; any finding aborts):
+#   make ubsan && VELES_SIMD_LIB=$PWD/build-ubsan/lib/libvelessimd.so VELES_DISABLE_GPU=1 \
+#     python -m pytest tests -m "not gpu" -p no:cacheprovider
+UBSAN_BUILD := build-ubsan
+UBSAN_RT    := $(dir $(shell /opt/rocm/lib/llvm/bin/clang -print-file-name=libclang_rt.ubsan_standalone-x86_64.so))
+ubsan:
+	$(MAKE) BUILD=$(UBSAN_BUILD) LIBDIR=$(UBSAN_BUILD)/lib LIB=$(UBSAN_BUILD)/lib/libvelessimd.so \
+	    OPT="-O1 -g -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined" \
+	    LDEXTRA="-fsanitize=undefined -shared-libsan -Wl,-rpath,$(UBSAN_RT)" lib
+
+.PHONY: ubsan
+
 # Host line coverage (gcov), the counterpart of the reference's
 # --enable-test-coverage (common.ac:229-236): host code of every source built
 # with --coverage, then the native C test and the CPU pytest suite run

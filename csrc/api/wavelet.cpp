@@ -17,15 +17,28 @@
 using vs::Staged;
 
 namespace {
-void check_dwt_args(const char *what, WaveletType type, int order,
-                    ExtensionType ext, const float *src, size_t length,
-                    const float *hi, const float *lo) {
+// The enum arguments come from C callers: their bits are read as an int and
+// checked before anything uses them as the C++ enum (loading an
+// out-of-range value through the enum type is undefined behaviour).
+template <class E>
+int enum_bits(const E &e) {
+  static_assert(sizeof(E) == sizeof(int), "C enum representation");
+  int v;
+  std::memcpy(&v, &e, sizeof(v));
+  return v;
+}
+
+#define VS_CHECK_DWT_ARGS(what) \
+  check_dwt_args(what, enum_bits(type), order, enum_bits(ext), src, length, desthi, destlo)
+
+void check_dwt_args(const char *what, int type, int order, int ext, const float *src,
+                    size_t length, const float *hi, const float *lo) {
   if (!src || !hi || !lo) vs::fatal("%s: null pointer", what);
-  if (!vs::wavelet_tables::valid(type, order))
-    vs::fatal("%s: unsupported wavelet (type %d, order %d)", what,
-              static_cast<int>(type), order);
+  if (type < WAVELET_TYPE_DAUBECHIES || type > WAVELET_TYPE_SYMLET ||
+      !vs::wavelet_tables::valid(static_cast<WaveletType>(type), order))
+    vs::fatal("%s: unsupported wavelet (type %d, order %d)", what, type, order);
   if (ext < EXTENSION_TYPE_PERIODIC || ext > EXTENSION_TYPE_ZERO)
-    vs::fatal("%s: bad extension type %d", what, static_cast<int>(ext));
+    vs::fatal("%s: bad extension type %d", what, ext);
   if (length == 0) vs::fatal("%s: empty source", what);
 }
 }  // namespace
@@ -69,7 +82,7 @@ void wavelet_recycle_source(int order, float *src, size_t length,
 void wavelet_apply_na(WaveletType type, int order, ExtensionType ext,
                       const float *src, size_t length, float *desthi,
                       float *destlo) {
-  check_dwt_args("wavelet_apply_na", type, order, ext, src, length, desthi, destlo);
+  VS_CHECK_DWT_ARGS("wavelet_apply_na");
   if (length % 2) vs::fatal("wavelet_apply_na: odd length %zu", length);
   vs::ref::dwt(type, order, ext, src, length, desthi, destlo);
 }
@@ -77,7 +90,7 @@ void wavelet_apply_na(WaveletType type, int order, ExtensionType ext,
 void wavelet_apply(WaveletType type, int order, ExtensionType ext,
                    const float *src, size_t length, float *desthi,
                    float *destlo) {
-  check_dwt_args("wavelet_apply", type, order, ext, src, length, desthi, destlo);
+  VS_CHECK_DWT_ARGS("wavelet_apply");
   if (length % 2) vs::fatal("wavelet_apply: odd length %zu", length);
   // Flag-less API (like arithmetic.h): GPU for device operands or enough
   // work (length x taps) to amortise the host<->device round trip.
@@ -102,8 +115,7 @@ void wavelet_apply(WaveletType type, int order, ExtensionType ext,
 void stationary_wavelet_apply_na(WaveletType type, int order, int level,
                                  ExtensionType ext, const float *src,
                                  size_t length, float *desthi, float *destlo) {
-  check_dwt_args("stationary_wavelet_apply_na", type, order, ext, src, length,
-                 desthi, destlo);
+  VS_CHECK_DWT_ARGS("stationary_wavelet_apply_na");
   if (level < 1) vs::fatal("stationary_wavelet_apply_na: level %d < 1", level);
   vs::ref::swt(type, order, level, ext, src, length, desthi, destlo);
 }
@@ -111,8 +123,7 @@ void stationary_wavelet_apply_na(WaveletType type, int order, int level,
 void stationary_wavelet_apply(WaveletType type, int order, int level,
                               ExtensionType ext, const float *src,
                               size_t length, float *desthi, float *destlo) {
-  check_dwt_args("stationary_wavelet_apply", type, order, ext, src, length,
-                 desthi, destlo);
+  VS_CHECK_DWT_ARGS("stationary_wavelet_apply");
   if (level < 1) vs::fatal("stationary_wavelet_apply: level %d < 1", level);
   if (!vs::api::use_gpu_array(length * order, {src, desthi, destlo})) {
     vs::host::swt(type, order, level, ext, src, length, desthi, destlo);
