@@ -28,7 +28,7 @@ def main():
     front = torch.nn.Linear(1024, 1024).to(dev)
     feats = models.WaveletEnergyFeatures(levels=4).to(dev)
     target = torch.tensor([4.0, 2.0, 1.0, 0.5, 0.25], device=dev)
-    opt = torch.optim.SGD(front.parameters(), lr=1e-3)
+    opt = torch.optim.SGD(front.parameters(), lr=0.5)
     for step in range(5):
         e = feats(front(x)).mean(0)                           # band energies, batch mean
         loss = ((e / e.sum() - target / target.sum()) ** 2).sum()
