@@ -428,8 +428,21 @@ struct Arena {
   int device = -1;
 };
 
-constexpr size_t kStageMax = 64 << 10;    // per operand
-constexpr size_t kArenaBytes = 4 << 20;   // per thread
+// Size of the image, per thread that calls the host API (VELES_STAGE_ARENA_MB).
+size_t arena_bytes() {
+  static const size_t v = static_cast<size_t>(env_int("VELES_STAGE_ARENA_MB", 16)) << 20;
+  return v;
+}
+constexpr size_t kEagerFlush = 128 << 10;  // a packed input this large is sent at once
+
+// Largest operand that is packed into the call's pinned image
+// (VELES_STAGE_MAX_KB).
+size_t stage_max() {
+  static const size_t v = static_cast<size_t>(env_int("VELES_STAGE_MAX_KB", 4096)) << 10;
+  return v;
+}
+
+constexpr size_t kPinnedInPlaceMin = 64 << 10;  // pinned operands above this skip the arena
 
 thread_local Arena t_arena;
 thread_local CallStaging *t_call = nullptr;
@@ -443,9 +456,9 @@ bool arena_ready() {
   if (a.dev) (void)hipFree(a.dev);
   a = Arena{};
   void *h = nullptr, *m = nullptr, *d = nullptr;
-  if (hipHostMalloc(&h, kArenaBytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+  if (hipHostMalloc(&h, arena_bytes(), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
-      hipHostGetDevicePointer(&m, h, 0) != hipSuccess || hipMalloc(&d, kArenaBytes) != hipSuccess) {
+      hipHostGetDevicePointer(&m, h, 0) != hipSuccess || hipMalloc(&d, arena_bytes()) != hipSuccess) {
     (void)hipGetLastError();
     if (h) (void)hipHostFree(h);
     return false;
@@ -453,7 +466,7 @@ bool arena_ready() {
   a.host = static_cast<char *>(h);
   a.mapped = static_cast<char *>(m);
   a.dev = static_cast<char *>(d);
-  a.cap = kArenaBytes;
+  a.cap = arena_bytes();
   a.device = dev;
   return true;
 }
@@ -470,7 +483,7 @@ CallStaging::~CallStaging() { t_call = prev_; }
 CallStaging *CallStaging::current() { return t_call; }
 
 void *CallStaging::reserve(const void *host_in, size_t bytes, bool zero_copy) {
-  if (bytes == 0 || bytes > kStageMax) return nullptr;
+  if (bytes == 0 || bytes > stage_max()) return nullptr;
   const size_t off = (used_ + 255) & ~size_t{255};
   if (!arena_ready() || off + bytes > t_arena.cap) return nullptr;
   used_ = off + bytes;
@@ -479,6 +492,8 @@ void *CallStaging::reserve(const void *host_in, size_t bytes, bool zero_copy) {
   if (host_in) {
     if (pend_hi_ == pend_lo_) pend_lo_ = off;
     pend_hi_ = off + bytes;
+    // the DMA of a large operand runs while the host packs the next one
+    if (bytes >= kEagerFlush) (void)flush();
   }
   return t_arena.dev + off;
 }
@@ -486,9 +501,10 @@ void *CallStaging::reserve(const void *host_in, size_t bytes, bool zero_copy) {
 vs_status CallStaging::flush() {
   if (pend_hi_ == pend_lo_) return VS_OK;
   const size_t lo = pend_lo_, n = pend_hi_ - pend_lo_;
-  pend_lo_ = pend_hi_ = 0;
+  // a failed copy stays pending, so the flush before the first kernel reports it
   VS_HIP(hipMemcpyAsync(t_arena.dev + lo, t_arena.host + lo, n, hipMemcpyHostToDevice,
                         stream_));
+  pend_lo_ = pend_hi_ = 0;
   return VS_OK;
 }
 
@@ -580,7 +596,7 @@ Staged::Staged(const void *user, size_t bytes, Dir dir, hipStream_t stream)
   // read-once inputs are read in place through the mapping, re-read inputs
   // and outputs move by asynchronous DMA -- truly asynchronous from pinned
   // memory; from pageable memory hipMemcpyAsync stages and blocks.
-  if (kind == MemKind::kPinned && bytes > kStageMax && !sync_stage()) {
+  if (kind == MemKind::kPinned && bytes > kPinnedInPlaceMin && !sync_stage()) {
     pinned_ = true;
     // read-once inputs and outputs use the mapping in place (an output
     // written through it overlaps the kernel: 300 x 256 x 1000 takes 82 us

@@ -136,11 +136,12 @@ bool scratch_refused_in_capture(size_t bytes, hipStream_t stream);
 
 // ----------------------------------------------------------- staging
 // Staging context of one host-API call (api::run_sync opens one per call).
-// Host operands of up to 64 KiB live in a pinned, device-mapped arena of the
+// Host operands of up to 4 MiB (VELES_STAGE_MAX_KB) live in a pinned, device-mapped arena of the
 // calling thread for the call: outputs and read-once inputs are accessed
 // there by the kernels directly (zero-copy); inputs re-read by many
 // workgroups (Staged::kReread) are packed and sent to a device arena with
-// ONE host->device copy before the first kernel reads them.  The call ends
+// ONE host->device copy before the first kernel reads them (inputs of
+// 128 KiB or more go at once, overlapping the packing of the next operand).  The call ends
 // with one event wait and the copies to the caller's buffers.  Larger
 // operands take the per-operand copy path; VELES_ZERO_COPY=0 moves every
 // small operand to the device arena.

@@ -57,11 +57,11 @@ const char *vs_last_error(void);
 int vs_is_device_pointer(const void *ptr);
 /// Pinned host memory for operands of the reference-compatible host API
 /// (<simd/matrix.h>, <simd/convolve.h>, ...).  Calls on pageable arrays
-/// copy every operand past 64 KiB through the runtime's staging buffers
-/// with the CPU (a 1 MiB memcpy costs more than its PCIe transfer); arrays
+/// copy every operand through the runtime's pinned staging image with the
+/// CPU (a 1 MiB memcpy costs more than its PCIe transfer); arrays
 /// from vs_host_alloc are recognised by the runtime: read-once inputs and
 /// outputs are accessed in place through the GPU mapping, re-read inputs
-/// move by asynchronous DMA (matrix_multiply 300 x 256 x 1000: 160 us on
+/// move by asynchronous DMA (matrix_multiply 300 x 256 x 1000: 114-127 us on
 /// pageable arrays, 82 us on pinned ones, of which the two PCIe transfers
 /// are the larger part).  Pinned tensors of other allocators (hipHostMalloc,
 /// torch pin_memory) are treated the same way.  Free with vs_host_free, not

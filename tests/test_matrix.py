@@ -248,3 +248,52 @@ def test_host_api_pinned_convolve():
         px[:] = x
         got = capi.convolve_simd(1, px, h)
     np.testing.assert_array_equal(got, want)
+
+
+_STAGE_LIMIT_CODE = r"""
+import numpy as np
+from veles.simd_amd import capi
+rng = np.random.default_rng(21)
+h1, w1, w2 = 300, 256, 1000                      # operands of 0.3, 1.0 and 1.2 MB
+a = rng.uniform(-1, 1, (h1, w1)).astype(np.float32)
+b = rng.uniform(-1, 1, (w1, w2)).astype(np.float32)
+ref = a.astype(np.float64) @ b.astype(np.float64)
+for rep in range(3):                             # the image is reused call after call
+    got = capi.matrix_multiply(1, a, b, w1, h1, w2, w1).reshape(h1, w2)
+    assert np.abs(got - ref).max() <= 2e-6 * w1, rep
+for n in (200, 700, 1500):                       # 0.16, 1.96 and 9 MB per operand
+    x = rng.standard_normal((n, n)).astype(np.float32)
+    y = rng.standard_normal((n, n)).astype(np.float32)
+    assert np.array_equal(capi.matrix_add(1, x, y, n, n), (x + y).ravel()), n
+    assert np.array_equal(capi.matrix_sub(1, x, y, n, n), (x - y).ravel()), n
+x = rng.standard_normal(300000).astype(np.float32)
+h = rng.standard_normal(500).astype(np.float32)
+want = np.convolve(x.astype(np.float64), h.astype(np.float64))
+assert np.abs(capi.convolve_simd(1, x, h) - want).max() <= 2e-3
+v = rng.uniform(0.1, 6.0, 262144).astype(np.float32)
+got = capi.psv("log_psv", 1, v).astype(np.float64)
+assert (np.abs(got - np.log(v.astype(np.float64))) <= 4e-7 * np.abs(np.log(v)) + 5e-7).all()
+print("stage-limit ok")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [
+    {},                                                        # 4 MiB operands in a 16 MiB image
+    {"VELES_STAGE_MAX_KB": "64"},                              # a pageable copy per large operand
+    {"VELES_STAGE_MAX_KB": "4096", "VELES_STAGE_ARENA_MB": "2"},   # image full after one operand
+    {"VELES_ZERO_COPY": "0"},                                  # outputs through the device image
+], ids=["default", "limit64k", "image2m", "no_zero_copy"])
+def test_host_api_staging_limits(env):
+    """Pageable operands below and above the limit of the pinned staging image
+    (VELES_STAGE_MAX_KB), with the image large, nearly full and bypassed: the
+    same results on every path."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, PYTHONPATH=repo + os.pathsep + os.environ.get("PYTHONPATH", ""), **env)
+    r = subprocess.run([sys.executable, "-c", _STAGE_LIMIT_CODE], env=e, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "stage-limit ok" in r.stdout

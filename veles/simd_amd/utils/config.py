@@ -37,6 +37,11 @@ KNOBS = [
          "csrc/runtime/runtime.cpp"),
     Knob("VELES_SYNC_STAGE", "0", "1: stage host operands with synchronous copies (debug)",
          "csrc/runtime/runtime.cpp"),
+    Knob("VELES_STAGE_MAX_KB", "4096", "largest pageable host operand (KiB) packed into the "
+         "call's pinned staging image; larger ones take a pageable copy each",
+         "csrc/runtime/runtime.cpp"),
+    Knob("VELES_STAGE_ARENA_MB", "16", "size of that image (pinned host + device), per thread "
+         "that calls the host API", "csrc/runtime/runtime.cpp"),
     Knob("VELES_ZERO_COPY", "1", "0: stage every small host operand into device memory "
          "instead of the mapped pinned arena", "csrc/runtime/runtime.cpp"),
     Knob("VELES_SGEMM_VARIANT", "-1", "force an SGEMM tile (0 / 1 / 2: 64 / 128 / 256 tiles "
