@@ -444,7 +444,31 @@ size_t stage_max() {
 
 constexpr size_t kPinnedInPlaceMin = 64 << 10;  // pinned operands above this skip the arena
 
-thread_local Arena t_arena;
+// Images of threads that have ended wait here for the next thread that needs
+// one: a program that calls the host API from short-lived threads holds as
+// many images as it has such threads at once, not one per thread it ever
+// started.  (No HIP call at thread exit: the main thread's exit may come
+// after the HIP runtime has shut down.)  Never destroyed, so that a thread
+// ending during process exit still finds it.
+struct ArenaPool {
+  std::mutex mu;
+  std::vector<Arena> idle;
+};
+ArenaPool &arena_pool() {
+  static ArenaPool *p = new ArenaPool;
+  return *p;
+}
+
+struct ThreadArena : Arena {
+  ~ThreadArena() {
+    if (!host) return;
+    ArenaPool &p = arena_pool();
+    std::lock_guard<std::mutex> lock(p.mu);
+    p.idle.push_back(*this);
+  }
+};
+
+thread_local ThreadArena t_arena;
 thread_local CallStaging *t_call = nullptr;
 
 bool arena_ready() {
@@ -452,9 +476,20 @@ bool arena_ready() {
   (void)hipGetDevice(&dev);
   Arena &a = t_arena;
   if (a.host && a.device == dev) return true;
-  if (a.host) (void)hipHostFree(a.host);
-  if (a.dev) (void)hipFree(a.dev);
-  a = Arena{};
+  ArenaPool &pool = arena_pool();
+  {
+    std::lock_guard<std::mutex> lock(pool.mu);
+    if (a.host) {  // this thread moved to another device
+      pool.idle.push_back(a);
+      a = Arena{};
+    }
+    for (size_t i = 0; i < pool.idle.size(); ++i)
+      if (pool.idle[i].device == dev && pool.idle[i].cap == arena_bytes()) {
+        a = pool.idle[i];
+        pool.idle.erase(pool.idle.begin() + static_cast<long>(i));
+        return true;
+      }
+  }
   void *h = nullptr, *m = nullptr, *d = nullptr;
   if (hipHostMalloc(&h, arena_bytes(), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||

@@ -84,3 +84,35 @@ def test_native_thread_test_binary():
     r = subprocess.run([exe, "8", "3"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failure(s)" in r.stdout
+
+
+@pytest.mark.gpu
+def test_short_lived_threads_reuse_staging_images():
+    """Threads that end hand their pinned staging image (16 MiB of pinned host
+    and of device memory) to the next thread that needs one: thirty threads in
+    a row, each making GPU calls on host arrays, hold one image between them."""
+    import torch
+    rng = np.random.default_rng(3)
+    big = rng.uniform(-1, 1, (200, 300)).astype(np.float32)
+    errors = []
+
+    def one():
+        try:
+            assert np.array_equal(capi.matrix_add(1, big, big, 300, 200), (big + big).ravel())
+        except BaseException as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    def spawn(n):
+        for _ in range(n):
+            t = threading.Thread(target=one)
+            t.start()
+            t.join()
+
+    spawn(2)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    spawn(30)
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert not errors, errors
+    assert free0 - free1 < (32 << 20), (free0, free1)   # 30 images would be 480 MiB
