@@ -8,6 +8,7 @@
 #include <cstring>
 
 #include "csrc/api/dispatch.h"
+#include "csrc/ref/ref.h"
 #include "simd/gpu.h"
 
 using vs::Staged;
@@ -208,7 +209,7 @@ void real_multiply_scalar(const float *array, size_t n, float value,
 }
 
 float sum_elements(const float *input, size_t n) {
-  if (!use_gpu_array(n, {input})) return sum_elements_na(input, n);
+  if (!use_gpu_array(n, {input})) return vs::host::sum_elements(input, n);
   float result = 0.f;
   run_sync("sum_elements", [&](hipStream_t s) {
     Staged x(input, n * 4, Staged::kIn, s);

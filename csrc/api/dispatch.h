@@ -44,16 +44,48 @@ inline bool use_gpu_simd(int simd, const char *fn) {
   return false;
 }
 
+// Limit for host_small() of calls that move more than they compute (sums and
+// differences, conversions, normalisation): on pageable host operands the
+// host loop is faster at every size, because the GPU path starts with a copy
+// of every operand into pinned memory that costs as much as the loop itself
+// (matrix_add 1024 x 1024: 100 us on the host, 480 us through the GPU).
+constexpr size_t kHostAlways = size_t{1} << 44;
+
 // simd != 0 calls on host operands whose work is below `limit` (elements or
 // multiply-adds, scaled by VELES_HOST_SMALL_SCALE percent) run vectorised host
 // loops: the GPU round trip alone costs 14-18 us.
 inline bool host_small(size_t work, size_t limit, std::initializer_list<const void *> ptrs) {
-  return work < limit * host_small_scale() / 100 && !any_device(ptrs);
+  const size_t scale = host_small_scale();
+  const bool below = limit >= kHostAlways ? scale != 0 : work < limit * scale / 100;
+  return below && !any_device(ptrs);
 }
 
+// True when the GPU thresholds of the flag-less API are the explicit ones:
+// VELES_GPU_MIN_ELEMS is set, or VELES_HOST_SMALL_SCALE is 0 (everything that
+// can run on the GPU does; the test suite runs so).
+inline bool explicit_gpu_threshold() {
+  return gpu_min_elems_is_set() || host_small_scale() == 0;
+}
+
+// Flag-less streaming calls (arithmetic.h: conversions, products, sums): the
+// GPU for device operands; for host operands only past an explicit threshold.
 inline bool use_gpu_array(size_t n, std::initializer_list<const void *> ptrs) {
   if (!gpu_available()) return false;
-  return n >= gpu_min_elems() || any_device(ptrs);
+  if (any_device(ptrs)) return true;
+  return explicit_gpu_threshold() && n >= gpu_min_elems();
+}
+
+// One wavelet level on host operands: the host filter bank costs about
+// 0.028 ns per sample and tap, the GPU path 20 us + 0.3 ns per sample (two
+// pinned copies and the PCIe transfers), so the GPU pays from about
+// length x (taps - 10) > 700,000 on (8 taps: never; 16 taps: 128 K samples;
+// 76 taps: 11 K samples).
+inline bool use_gpu_wavelet(size_t length, int order, std::initializer_list<const void *> ptrs) {
+  if (!gpu_available()) return false;
+  if (any_device(ptrs)) return true;
+  if (explicit_gpu_threshold()) return length * static_cast<size_t>(order) >= gpu_min_elems();
+  const size_t over = order > 10 ? static_cast<size_t>(order - 10) : 0;
+  return length * over > 700000 * host_small_scale() / 100;
 }
 
 // Runs body(stream) on the library stream and waits for it; aborts with the

@@ -10,9 +10,9 @@
 #include "simd/gpu.h"
 
 namespace {
-// Arrays this short run libm on the host even with simd = 1 (about 10 ns per
-// element against a GPU round trip of 14-18 us).
-constexpr size_t kSmallElems = 1024;
+// Arrays this short run libm on the host even with simd = 1 (1.3 ns per
+// element for logf against a GPU round trip of 13-16 us).
+constexpr size_t kSmallElems = 8192;
 
 void psv(int simd, int fn, const char *what, PsvStdFunc host, const float *src,
          size_t n, float *res) {

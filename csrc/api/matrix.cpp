@@ -12,7 +12,7 @@ using vs::Staged;
 namespace {
 // Work below which a simd = 1 call on host operands stays on the host
 // (a GPU round trip is 14-18 us; the host loops run 4-16 floats per cycle).
-constexpr size_t kSmallElems = 16384;  // add / sub, elements
+constexpr size_t kSmallElems = vs::api::kHostAlways;  // add / sub: host operands stay on the host
 constexpr size_t kSmallMacs = 65536;   // multiply, multiply-adds
 
 void elementwise(int simd, int op, const char *what, const float *m1,

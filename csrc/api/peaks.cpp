@@ -11,6 +11,10 @@
 
 using vs::Staged;
 
+namespace {
+constexpr size_t kSmallElems = 262144;  // noise (two of three samples an extremum): 108 us per 128 K on the host, 190 us through the GPU
+}
+
 extern "C" {
 
 void detect_peaks(int simd, const float *data, size_t size, ExtremumType type,
@@ -20,10 +24,14 @@ void detect_peaks(int simd, const float *data, size_t size, ExtremumType type,
   *results = nullptr;
   *resultsLength = 0;
   // short arrays stay on the host: two GPU round trips (count, then emit)
-  // cost more than the scan
-  if (!vs::api::use_gpu_simd(simd, "detect_peaks") ||
-      vs::api::host_small(size, 16384, {data})) {
+  // cost more than the two-pass host scan (about 1 ns per element)
+  if (!simd) {
     vs::ref::detect_peaks(data, size, type, results, resultsLength);
+    return;
+  }
+  if (!vs::api::use_gpu_simd(simd, "detect_peaks") ||
+      vs::api::host_small(size, kSmallElems, {data})) {
+    vs::host::detect_peaks(data, size, type, results, resultsLength);
     return;
   }
   unsigned long long total = 0;

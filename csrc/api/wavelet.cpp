@@ -93,8 +93,8 @@ void wavelet_apply(WaveletType type, int order, ExtensionType ext,
   VS_CHECK_DWT_ARGS("wavelet_apply");
   if (length % 2) vs::fatal("wavelet_apply: odd length %zu", length);
   // Flag-less API (like arithmetic.h): GPU for device operands or enough
-  // work (length x taps) to amortise the host<->device round trip.
-  if (!vs::api::use_gpu_array(length * order, {src, desthi, destlo})) {
+  // work per sample moved to amortise the host<->device round trip.
+  if (!vs::api::use_gpu_wavelet(length, order, {src, desthi, destlo})) {
     vs::host::dwt(type, order, ext, src, length, desthi, destlo);
     return;
   }
@@ -125,7 +125,7 @@ void stationary_wavelet_apply(WaveletType type, int order, int level,
                               size_t length, float *desthi, float *destlo) {
   VS_CHECK_DWT_ARGS("stationary_wavelet_apply");
   if (level < 1) vs::fatal("stationary_wavelet_apply: level %d < 1", level);
-  if (!vs::api::use_gpu_array(length * order, {src, desthi, destlo})) {
+  if (!vs::api::use_gpu_wavelet(length, order, {src, desthi, destlo})) {
     vs::host::swt(type, order, level, ext, src, length, desthi, destlo);
     return;
   }

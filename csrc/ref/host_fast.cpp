@@ -8,8 +8,13 @@
 // (reference src/convolve.c:49-100, src/wavelet.c:395-1555).
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#endif
 
 #include "csrc/data/wavelet_tables.h"
 #include "csrc/ref/ref.h"
@@ -137,6 +142,52 @@ VS_BODY void dot_body(const float *__restrict__ a, const float *__restrict__ b, 
   *out = r;
 }
 
+// sum with 4 x 8 partial sums (the scalar loop is one dependent add per element)
+VS_BODY void sum_body(const float *__restrict__ a, long n, float *__restrict__ out) {
+  V8 s0 = {}, s1 = {}, s2 = {}, s3 = {};
+  long i = 0;
+  for (; i + 32 <= n; i += 32) {
+    s0 += *reinterpret_cast<const V8u *>(a + i);
+    s1 += *reinterpret_cast<const V8u *>(a + i + 8);
+    s2 += *reinterpret_cast<const V8u *>(a + i + 16);
+    s3 += *reinterpret_cast<const V8u *>(a + i + 24);
+  }
+  const V8 s = (s0 + s1) + (s2 + s3);
+  float r = ((s[0] + s[4]) + (s[1] + s[5])) + ((s[2] + s[6]) + (s[3] + s[7]));
+  for (; i < n; i++) r += a[i];
+  *out = r;
+}
+
+// smallest and largest element; NaNs lose every comparison, as in the scalar loop
+VS_BODY void minmax_body(const float *__restrict__ a, long n, float *__restrict__ out) {
+  float lo = a[0], hi = a[0];
+  long i = 0;
+  if (n >= 16) {
+    V8 l0, l1, h0, h1;
+    for (int k = 0; k < 8; k++) l0[k] = l1[k] = h0[k] = h1[k] = a[0];
+    for (; i + 16 <= n; i += 16) {
+      const V8 u = *reinterpret_cast<const V8u *>(a + i);
+      const V8 v = *reinterpret_cast<const V8u *>(a + i + 8);
+      l0 = u < l0 ? u : l0;
+      h0 = u > h0 ? u : h0;
+      l1 = v < l1 ? v : l1;
+      h1 = v > h1 ? v : h1;
+    }
+    for (int k = 0; k < 8; k++) {
+      if (l0[k] < lo) lo = l0[k];
+      if (l1[k] < lo) lo = l1[k];
+      if (h0[k] > hi) hi = h0[k];
+      if (h1[k] > hi) hi = h1[k];
+    }
+  }
+  for (; i < n; i++) {
+    if (a[i] < lo) lo = a[i];
+    if (a[i] > hi) hi = a[i];
+  }
+  out[0] = lo;
+  out[1] = hi;
+}
+
 bool have_avx2() {
 #if VS_HOST_AVX2
   static const bool yes = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
@@ -163,6 +214,8 @@ VS_DISPATCH(split, (const float *src, long half, float *ev, float *od), (src, ha
 VS_DISPATCH(addsub, (const float *a, const float *b, float sign, float *out, long n),
             (a, b, sign, out, n))
 VS_DISPATCH(dot, (const float *a, const float *b, long n, float *out), (a, b, n, out))
+VS_DISPATCH(sum, (const float *a, long n, float *out), (a, n, out))
+VS_DISPATCH(minmax, (const float *a, long n, float *out), (a, n, out))
 #undef VS_DISPATCH
 
 float extended(const float *src, long len, long idx, ExtensionType ext) {
@@ -274,6 +327,85 @@ void matrix_add(const float *a, const float *b, size_t w, size_t h, float *res) 
 
 void matrix_sub(const float *a, const float *b, size_t w, size_t h, float *res) {
   addsub(a, b, -1.f, res, static_cast<long>(w * h));
+}
+
+float sum_elements(const float *a, size_t n) {
+  float r = 0.f;
+  sum(a, static_cast<long>(n), &r);
+  return r;
+}
+
+void minmax1d(const float *src, size_t n, float *mn, float *mx) {
+  float out[2];
+  minmax(src, static_cast<long>(n), out);
+  if (mn) *mn = out[0];
+  if (mx) *mx = out[1];
+}
+
+#if VS_HOST_AVX2
+// Extrema of the kinds in `type` among x[1 .. n - 2], eight positions per
+// step: the tests of the scalar loop as lane masks, one bit per position.
+// With pts == nullptr the extrema are only counted.
+VS_TARGET_AVX2 long peaks_avx2(const float *x, long n, int type, ExtremumPoint *pts) {
+  const __m256 zero = _mm256_setzero_ps();
+  const __m256 want_max = _mm256_castsi256_ps(
+      _mm256_set1_epi32((type & kExtremumTypeMaximum) ? -1 : 0));
+  const __m256 want_min = _mm256_castsi256_ps(
+      _mm256_set1_epi32((type & kExtremumTypeMinimum) ? -1 : 0));
+  long k = 0, i = 1;
+  for (; i + 8 < n; i += 8) {
+    const __m256 c = _mm256_loadu_ps(x + i);
+    const __m256 d1 = _mm256_sub_ps(c, _mm256_loadu_ps(x + i - 1));
+    const __m256 d2 = _mm256_sub_ps(c, _mm256_loadu_ps(x + i + 1));
+    const __m256 ext = _mm256_cmp_ps(_mm256_mul_ps(d1, d2), zero, _CMP_GT_OQ);
+    const __m256 kind = _mm256_or_ps(
+        _mm256_and_ps(_mm256_cmp_ps(d1, zero, _CMP_GT_OQ), want_max),
+        _mm256_and_ps(_mm256_cmp_ps(d1, zero, _CMP_LT_OQ), want_min));
+    unsigned m = static_cast<unsigned>(_mm256_movemask_ps(_mm256_and_ps(ext, kind)));
+    if (!pts) {
+      k += __builtin_popcount(m);
+      continue;
+    }
+    while (m) {
+      const long p = i + __builtin_ctz(m);
+      pts[k++] = ExtremumPoint{static_cast<int>(p), x[p]};
+      m &= m - 1;
+    }
+  }
+  for (; i + 1 < n; i++) {
+    const float d1 = x[i] - x[i - 1], d2 = x[i] - x[i + 1];
+    if (d1 * d2 > 0 && ((d1 > 0 && (type & kExtremumTypeMaximum)) ||
+                        (d1 < 0 && (type & kExtremumTypeMinimum)))) {
+      if (pts) pts[k] = ExtremumPoint{static_cast<int>(i), x[i]};
+      k++;
+    }
+  }
+  return k;
+}
+#endif
+
+// Two passes, count then write, so that the result is allocated once at its
+// final size and no pass branches on the data.
+void detect_peaks(const float *x, size_t n, ExtremumType type, ExtremumPoint **out,
+                  size_t *count) {
+#if VS_HOST_AVX2
+  if (have_avx2()) {
+    const long c = peaks_avx2(x, static_cast<long>(n), static_cast<int>(type), nullptr);
+    *count = static_cast<size_t>(c);
+    *out = nullptr;
+    if (c == 0) return;
+    auto *pts = static_cast<ExtremumPoint *>(
+        std::malloc(static_cast<size_t>(c) * sizeof(ExtremumPoint)));
+    if (!pts) {
+      *count = 0;
+      return;
+    }
+    peaks_avx2(x, static_cast<long>(n), static_cast<int>(type), pts);
+    *out = pts;
+    return;
+  }
+#endif
+  ref::detect_peaks(x, n, type, out, count);
 }
 
 // res (h1 x w2) = a (h1 x w1) b (w1 x w2): row i of res accumulates

@@ -68,6 +68,10 @@ void dwt(WaveletType type, int order, ExtensionType ext, const float *src, size_
          float *hi, float *lo);
 void swt(WaveletType type, int order, int level, ExtensionType ext, const float *src,
          size_t len, float *hi, float *lo);
+float sum_elements(const float *a, size_t n);
+void minmax1d(const float *src, size_t n, float *mn, float *mx);
+void detect_peaks(const float *x, size_t n, ExtremumType type, ExtremumPoint **out,
+                  size_t *count);
 void matrix_add(const float *a, const float *b, size_t w, size_t h, float *res);
 void matrix_sub(const float *a, const float *b, size_t w, size_t h, float *res);
 void matrix_multiply(const float *a, const float *b, size_t w1, size_t h1, size_t w2,

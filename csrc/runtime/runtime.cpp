@@ -150,6 +150,14 @@ size_t gpu_min_elems() {
   return n;
 }
 
+bool gpu_min_elems_is_set() {
+  static const bool set = [] {
+    const char *v = std::getenv("VELES_GPU_MIN_ELEMS");
+    return v && *v;
+  }();
+  return set;
+}
+
 size_t host_small_scale() {
   static const size_t n = [] {
     const char *v = std::getenv("VELES_HOST_SMALL_SCALE");

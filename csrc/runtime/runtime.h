@@ -81,8 +81,9 @@ int device_count();
 hipStream_t library_stream();
 bool is_device_pointer(const void *p);
 // Elements from which host-pointer array ops go to the GPU
-// (VELES_GPU_MIN_ELEMS, default 1 << 20).
+// (VELES_GPU_MIN_ELEMS; 1 << 20 when unset, see api::explicit_gpu_threshold).
 size_t gpu_min_elems();
+bool gpu_min_elems_is_set();
 // Percent applied to the small-call host limits of the simd = 1 host API
 // (VELES_HOST_SMALL_SCALE, default 100; 0 sends every such call to the GPU).
 size_t host_small_scale();

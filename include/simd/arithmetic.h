@@ -6,9 +6,11 @@
  *  exported library functions with two execution paths:
  *   - array functions (conversions, *_array, complex_conjugate,
  *     real_multiply_scalar, sum_elements, add_to_all) run as HIP kernels when
- *     their operands live in device memory or when the array is large enough
- *     for the GPU to win (VELES_GPU_MIN_ELEMS, default 1 Mi elements), and on
- *     the host otherwise;
+ *     an operand lives in device memory, and as host loops otherwise: on
+ *     host arrays one pass of the CPU costs less than the copy into pinned
+ *     memory the GPU path starts with (real_multiply_array over 1 Mi floats:
+ *     108 us on the host, 490 us through the GPU).  VELES_GPU_MIN_ELEMS=n
+ *     sends host arrays of n elements or more to the GPU all the same;
  *   - the fixed-width "register" helpers (real_multiply, complex_multiply,
  *     complex_multiply_conjugate: FLOAT_STEP floats; int16_multiply:
  *     INT16MUL_STEP elements) are host helpers with the reference AVX2

@@ -121,16 +121,82 @@ def test_small_matrix_and_math_calls_run_host_loops():
     assert "done on GPU" not in out
 
 
+_STREAMING_CALLS = r"""
+import ctypes
+import numpy as np
+from veles.simd_amd import capi
+rng = np.random.default_rng(9)
+sz = ctypes.c_size_t
+# sums and differences, conversions, products: the host at every size
+n = 1500
+a = rng.standard_normal((n, n)).astype(np.float32)
+b = rng.standard_normal((n, n)).astype(np.float32)
+np.testing.assert_array_equal(capi.matrix_add(1, a, b, n, n), (a + b).ravel())
+np.testing.assert_array_equal(capi.matrix_sub(1, a, b, n, n), (a - b).ravel())
+m = (1 << 21) + 7
+x, y, z = a.ravel()[:m], b.ravel()[:m], np.empty(m, np.float32)
+capi.fn("real_multiply_array")(capi.p(x), capi.p(y), sz(m), capi.p(z))
+np.testing.assert_array_equal(z, x * y)
+i16 = rng.integers(-30000, 30000, m).astype(np.int16)
+capi.fn("int16_to_float")(capi.p(i16), sz(m), capi.p(z))
+np.testing.assert_array_equal(z, i16.astype(np.float32))
+# reductions: eight-lane partial sums / lane-wise extremes
+for k in (1, 7, 15, 16, 31, 32, 33, 1000, m):
+    v = x[:k]
+    got = capi.fn("sum_elements")(capi.p(v), sz(k))
+    want = float(v.astype(np.float64).sum())
+    assert abs(got - want) <= 2e-6 * float(np.abs(v).astype(np.float64).sum()) + 1e-6, (k, got, want)
+    lo, hi = ctypes.c_float(), ctypes.c_float()
+    capi.fn("minmax1D")(1, capi.p(v), k, ctypes.byref(lo), ctypes.byref(hi))
+    assert (lo.value, hi.value) == (v.min(), v.max()), k
+w = x[:100].copy(); w[17] = np.nan                       # NaNs lose every comparison
+lo, hi = ctypes.c_float(), ctypes.c_float()
+capi.fn("minmax1D")(1, capi.p(w), 100, ctypes.byref(lo), ctypes.byref(hi))
+l0, h0 = ctypes.c_float(), ctypes.c_float()
+capi.fn("minmax1D")(0, capi.p(w), 100, ctypes.byref(l0), ctypes.byref(h0))
+assert (lo.value, hi.value) == (l0.value, h0.value)
+# normalisation
+img = rng.integers(0, 256, (700, 900), dtype=np.uint8)
+n1, n0 = np.empty((700, 900), np.float32), np.empty((700, 900), np.float32)
+capi.fn("normalize2D")(1, capi.p(img), 900, 900, 700, capi.p(n1), 900)
+capi.fn("normalize2D")(0, capi.p(img), 900, 900, 700, capi.p(n0), 900)
+np.testing.assert_array_equal(n1, n0)
+# extrema: two-pass host scan, every kind, plateaus and short arrays
+for k in (3, 4, 5, 64, 1000, 100000):
+    sig = np.round(rng.standard_normal(k) * 3).astype(np.float32)   # many equal neighbours
+    for kind in (1, 2, 3):
+        assert capi.detect_peaks(1, sig, kind) == capi.detect_peaks(0, sig, kind), (k, kind)
+# eight-tap wavelets stay on the host at any length
+src = rng.standard_normal(1 << 19).astype(np.float32)
+hi1, lo1 = capi.wavelet_apply(0, 8, 0, src)
+hi0, lo0 = capi.wavelet_apply(0, 8, 0, src, na=True)
+np.testing.assert_allclose(hi1, hi0, atol=2e-5)
+np.testing.assert_allclose(lo1, lo0, atol=2e-5)
+print("streaming calls ok")
+"""
+
+
+def test_streaming_calls_on_host_arrays_stay_on_the_host():
+    """Default policy: calls that move more than they compute never take the GPU round trip
+    for host operands, whatever their size (on a GPU box too), and match the scalar paths."""
+    out = _child(_STREAMING_CALLS, VELES_LOG_LEVEL="2")
+    assert "streaming calls ok" in out
+    assert "done on GPU" not in out
+
+
 @pytest.mark.gpu
 def test_larger_calls_still_reach_the_gpu():
     code = r"""
 import numpy as np
 from veles.simd_amd import capi
 a = np.ones((200, 200), np.float32)
-capi.matrix_add(1, a, a, 200, 200)
 capi.matrix_multiply(1, a, a, 200, 200, 200, 200)
-capi.psv("sin_psv", 1, np.ones(5000, np.float32))
+capi.psv("sin_psv", 1, np.ones(20000, np.float32))
+capi.detect_peaks(1, np.random.default_rng(0).standard_normal(400000).astype(np.float32), 3)
+capi.wavelet_apply(0, 16, 0, np.ones(1 << 18, np.float32))
+capi.wavelet_apply(0, 76, 0, np.ones(1 << 14, np.float32))
 """
     out = _child(code, VELES_LOG_LEVEL="2")
-    for what in ("matrix_add", "matrix_multiply", "sin_psv"):
+    for what in ("matrix_multiply", "sin_psv", "detect_peaks", "wavelet_apply"):
         assert f"{what}: done on GPU" in out
+    assert out.count("wavelet_apply: done on GPU") == 2

@@ -28,8 +28,10 @@ KNOBS = [
          "(native stderr)", "csrc/runtime/runtime.cpp"),
     Knob("VELES_DISABLE_GPU", "0", "1: behave as if no GPU were present (host reference "
          "paths)", "csrc/runtime/runtime.cpp"),
-    Knob("VELES_GPU_MIN_ELEMS", str(1 << 20), "host arrays of at least this many elements "
-         "(x taps for wavelets) run on the GPU in the flag-less API", "csrc/runtime/runtime.cpp"),
+    Knob("VELES_GPU_MIN_ELEMS", "", "when set: host arrays of at least this many elements "
+         "(x taps for wavelets) run on the GPU in the flag-less API; unset, streaming calls on "
+         "host arrays stay on the host (1048576 applies when VELES_HOST_SMALL_SCALE=0)",
+         "csrc/runtime/runtime.cpp"),
     Knob("VELES_HOST_MAX_MACS", str(1 << 19), "convolutions of host operands (direct calls and handles) "
          "below this many multiply-adds run on the host even with simd=1", "csrc/api/convolve.cpp"),
     Knob("VELES_HOST_SMALL_SCALE", "100", "percent applied to the small-call limits below which "
