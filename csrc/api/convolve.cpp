@@ -69,7 +69,7 @@ void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl
 size_t host_max_macs() {
   static const size_t v = [] {
     const char *e = std::getenv("VELES_HOST_MAX_MACS");
-    return e && *e ? static_cast<size_t>(std::atoll(e)) : static_cast<size_t>(1) << 19;
+    return e && *e ? static_cast<size_t>(std::atoll(e)) : static_cast<size_t>(3) << 18;
   }();
   return v;
 }

@@ -71,6 +71,17 @@ def child():
     for n in (1 << 10, 1 << 12, 1 << 14):
         x, y = np.abs(f(n)) + 0.1, f(n)
         case(f"log_psv {n}", "log_psv", (x, y), 1, capi.p(x), sz(n), capi.p(y))
+    for n in (32, 48, 64, 96, 128):
+        x, y, z = f(n * n), f(n * n), f(n * n)
+        case(f"matrix_multiply {n}^3", "matrix_multiply", (x, y, z), 1, capi.p(x), capi.p(y), n, n,
+             n, n, capi.p(z))
+    for n, k in ((1024, 256), (1024, 512), (2048, 512), (4096, 512), (65536, 16), (65536, 64)):
+        x, h, y = f(n), f(k), f(n + k - 1)
+        case(f"convolve_simd {n}x{k}", "convolve_simd", (x, h, y), 1, capi.p(x), sz(n), capi.p(h),
+             sz(k), capi.p(y))
+    only = os.environ.get("ONLY")
+    if only:
+        cases = {k: v for k, v in cases.items() if any(o in k for o in only.split(","))}
     out = {}
     for name, (fn, _keep) in cases.items():
         for _ in range(5):

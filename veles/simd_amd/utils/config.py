@@ -32,7 +32,7 @@ KNOBS = [
          "(x taps for wavelets) run on the GPU in the flag-less API; unset, streaming calls on "
          "host arrays stay on the host (1048576 applies when VELES_HOST_SMALL_SCALE=0)",
          "csrc/runtime/runtime.cpp"),
-    Knob("VELES_HOST_MAX_MACS", str(1 << 19), "convolutions of host operands (direct calls and handles) "
+    Knob("VELES_HOST_MAX_MACS", str(3 << 18), "convolutions of host operands (direct calls and handles) "
          "below this many multiply-adds run on the host even with simd=1", "csrc/api/convolve.cpp"),
     Knob("VELES_HOST_SMALL_SCALE", "100", "percent applied to the small-call limits below which "
          "simd=1 matrix / math calls on host operands run host loops (0: always the GPU)",
