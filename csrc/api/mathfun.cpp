@@ -22,6 +22,12 @@ void psv(int simd, int fn, const char *what, PsvStdFunc host, const float *src,
     return;
   }
   vs::api::run_sync(what, [&](hipStream_t s) {
+    const vs::MapArray arrays[] = {{src, nullptr, 4}, {nullptr, res, 4}};
+    vs_status piped = VS_OK;
+    if (vs::pipelined_map(s, n, arrays, 2, [&](void *const *d, size_t cnt, hipStream_t st) {
+          return vs_math(fn, static_cast<const float *>(d[0]), static_cast<float *>(d[1]), cnt, st);
+        }, &piped))
+      return piped;
     vs::Staged o(res, n * 4, vs::Staged::kOut, s);
     vs::Staged x(src, n * 4, vs::Staged::kIn, s);
     VS_TRY(o.status());
@@ -56,6 +62,13 @@ void sincos_psv(int simd, const float *src, size_t n, float *s, float *c) {
     return;
   }
   vs::api::run_sync("sincos_psv", [&](hipStream_t st) {
+    const vs::MapArray arrays[] = {{src, nullptr, 4}, {nullptr, s, 4}, {nullptr, c, 4}};
+    vs_status piped = VS_OK;
+    if (vs::pipelined_map(st, n, arrays, 3, [&](void *const *d, size_t cnt, hipStream_t q) {
+          return vs_sincos(static_cast<const float *>(d[0]), static_cast<float *>(d[1]),
+                           static_cast<float *>(d[2]), cnt, q);
+        }, &piped))
+      return piped;
     vs::Staged os(s, n * 4, vs::Staged::kOut, st);
     vs::Staged oc(c, n * 4, vs::Staged::kOut, st);
     vs::Staged x(src, n * 4, vs::Staged::kIn, st);
@@ -75,6 +88,13 @@ void pow_psv(int simd, const float *x, const float *y, size_t n, float *res) {
     return;
   }
   vs::api::run_sync("pow_psv", [&](hipStream_t st) {
+    const vs::MapArray arrays[] = {{x, nullptr, 4}, {y, nullptr, 4}, {nullptr, res, 4}};
+    vs_status piped = VS_OK;
+    if (vs::pipelined_map(st, n, arrays, 3, [&](void *const *d, size_t cnt, hipStream_t q) {
+          return vs_pow(static_cast<const float *>(d[0]), static_cast<const float *>(d[1]),
+                        static_cast<float *>(d[2]), cnt, q);
+        }, &piped))
+      return piped;
     vs::Staged o(res, n * 4, vs::Staged::kOut, st);
     vs::Staged a(x, n * 4, vs::Staged::kIn, st);
     vs::Staged b(y, n * 4, vs::Staged::kIn, st);

@@ -571,24 +571,12 @@ vs_status CallStaging::complete() {
   return VS_OK;
 }
 
-vs_status wait_stream(hipStream_t s) {
-  thread_local hipEvent_t ev = nullptr;
-  thread_local int ev_dev = -1;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (ev && ev_dev != dev) {
-    (void)hipEventDestroy(ev);
-    ev = nullptr;
-  }
-  if (!ev) {
-    VS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    ev_dev = dev;
-  }
-  VS_HIP(hipEventRecord(ev, s));
-  // Short calls (the common host-API case, ~10 us) are caught by polling: a
-  // blocking wait adds the wake-up latency of the interrupt path.  Past
-  // kSpinUs the call is long enough not to care, and a blocking wait frees
-  // the core for other host threads.
+namespace {
+// Short waits (the common host-API case, ~10 us) are caught by polling: a
+// blocking wait adds the wake-up latency of the interrupt path.  Past
+// kSpinUs the wait is long enough not to care, and a blocking wait frees
+// the core for other host threads.
+vs_status wait_event(hipEvent_t ev) {
   constexpr long kSpinUs = 50;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
@@ -601,6 +589,34 @@ vs_status wait_stream(hipStream_t s) {
   }
   VS_HIP(hipEventSynchronize(ev));
   return VS_OK;
+}
+
+// Events of the calling thread on the current device: 0 for wait_stream, 1
+// and 2 for the two halves of the staging image in pipelined_map.
+vs_status thread_event(int which, hipEvent_t *out) {
+  thread_local hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  thread_local int ev_dev = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (ev_dev != dev) {
+    for (hipEvent_t &e : ev)
+      if (e) {
+        (void)hipEventDestroy(e);
+        e = nullptr;
+      }
+    ev_dev = dev;
+  }
+  if (!ev[which]) VS_HIP(hipEventCreateWithFlags(&ev[which], hipEventDisableTiming));
+  *out = ev[which];
+  return VS_OK;
+}
+}  // namespace
+
+vs_status wait_stream(hipStream_t s) {
+  hipEvent_t ev = nullptr;
+  VS_TRY(thread_event(0, &ev));
+  VS_HIP(hipEventRecord(ev, s));
+  return wait_event(ev);
 }
 
 // What the runtime knows about a pointer: device memory, host memory it has
@@ -701,6 +717,75 @@ vs_status Staged::finish() {
   else
     VS_HIP(hipMemcpyAsync(user_, dev_, bytes_, hipMemcpyDeviceToHost, stream_));
   return VS_OK;
+}
+
+bool pipelined_map(hipStream_t s, size_t n, const MapArray *arrays, int count,
+                   const MapLaunch &launch, vs_status *status) {
+  constexpr size_t kPieceElems = 256 << 10;  // 1 MiB of floats per array and piece
+  constexpr int kMaxArrays = 8;
+  static const bool enabled = env_int("VELES_PIPELINED_MAP", 1) != 0;
+  *status = VS_OK;
+  if (!enabled || n < 2 * kPieceElems || count > kMaxArrays || sync_stage() ||
+      !zero_copy_enabled())
+    return false;
+  size_t per_elem = 0;
+  for (int i = 0; i < count; i++) {
+    void *mapped = nullptr;
+    const void *p = arrays[i].in ? arrays[i].in : arrays[i].out;
+    if (classify(p, &mapped) != MemKind::kPageable) return false;
+    per_elem += arrays[i].elem;
+  }
+  if (!arena_ready()) return false;
+  const Arena &a = t_arena;
+  const size_t half = a.cap / 2;
+  size_t piece = kPieceElems;
+  const size_t fit = (half - 256 * static_cast<size_t>(count)) / per_elem;
+  if (fit < piece) piece = fit & ~size_t{63};
+  if (piece == 0) return false;
+  // offsets of the arrays inside one half
+  size_t off[kMaxArrays];
+  size_t cur = 0;
+  for (int i = 0; i < count; i++) {
+    off[i] = cur;
+    cur += (piece * arrays[i].elem + 255) & ~size_t{255};
+  }
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  if ((*status = thread_event(1, &ev[0])) != VS_OK) return true;
+  if ((*status = thread_event(2, &ev[1])) != VS_OK) return true;
+  const size_t pieces = (n + piece - 1) / piece;
+  log(2, "pipelined map: %zu elements in %zu pieces of %zu", n, pieces, piece);
+  // step c: retire piece c - 2 (same half), then fill and launch piece c
+  for (size_t c = 0; c < pieces + 2; c++) {
+    const size_t h = (c & 1) * half;
+    if (c >= 2) {
+      const size_t first = (c - 2) * piece, cnt = std::min(piece, n - first);
+      if ((*status = wait_event(ev[c & 1])) != VS_OK) break;
+      for (int i = 0; i < count; i++)
+        if (arrays[i].out)
+          std::memcpy(static_cast<char *>(arrays[i].out) + first * arrays[i].elem,
+                      a.host + h + off[i], cnt * arrays[i].elem);
+    }
+    if (c < pieces) {
+      const size_t first = c * piece, cnt = std::min(piece, n - first);
+      void *dev[kMaxArrays];
+      for (int i = 0; i < count; i++) {
+        if (arrays[i].in)
+          std::memcpy(a.host + h + off[i],
+                      static_cast<const char *>(arrays[i].in) + first * arrays[i].elem,
+                      cnt * arrays[i].elem);
+        dev[i] = a.mapped + h + off[i];
+      }
+      if ((*status = launch(dev, cnt, s)) != VS_OK) break;
+      const hipError_t e = hipEventRecord(ev[c & 1], s);
+      if (e != hipSuccess) {
+        *status = hip_status(e, "hipEventRecord", __FILE__, __LINE__);
+        break;
+      }
+    }
+  }
+  // on an error, nothing may still be using the image when the caller goes on
+  if (*status != VS_OK) (void)hipStreamSynchronize(s);
+  return true;
 }
 
 }  // namespace vs

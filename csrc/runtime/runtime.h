@@ -11,6 +11,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -211,5 +212,25 @@ class Staged {
 // Waits for everything queued on `s` so far by polling an event (lower
 // latency than a blocking stream synchronise on a short call).
 vs_status wait_stream(hipStream_t s);
+
+// Element-wise maps over long pageable host arrays, in pieces through the two
+// halves of the calling thread's pinned staging image: while the GPU works on
+// one piece (reading and writing the image in place over the host link), the
+// host copies the previous piece's results out and the next piece's inputs
+// in.  A whole-array pass costs about 90 us per MiB (copy in, transfer and
+// kernel, copy out, one after the other); the pieces overlap the three.
+struct MapArray {
+  const void *in;  // input array, or nullptr for an output
+  void *out;       // output array, or nullptr for an input
+  size_t elem;     // bytes per element
+};
+// launch(dev, count, stream) gets one device-visible pointer per array, in
+// the order given, for `count` elements.
+using MapLaunch = std::function<vs_status(void *const *dev, size_t count, hipStream_t s)>;
+// False (and nothing done) when the pieces do not apply: an array in device
+// or pinned memory, fewer than two pieces, staging switched to synchronous or
+// device copies, or no image; the caller then takes the whole-array path.
+bool pipelined_map(hipStream_t s, size_t n, const MapArray *arrays, int count,
+                   const MapLaunch &launch, vs_status *status);
 
 }  // namespace vs

@@ -273,6 +273,21 @@ assert np.abs(capi.convolve_simd(1, x, h) - want).max() <= 2e-3
 v = rng.uniform(0.1, 6.0, 262144).astype(np.float32)
 got = capi.psv("log_psv", 1, v).astype(np.float64)
 assert (np.abs(got - np.log(v.astype(np.float64))) <= 4e-7 * np.abs(np.log(v)) + 5e-7).all()
+# long maps go through the image in pieces of 262,144 elements, two in flight
+for n in (2 * 262144, 3 * 262144 + 77, 5 * 262144 - 1):
+    v = rng.uniform(0.1, 6.0, n).astype(np.float32)
+    w = rng.uniform(-2.0, 2.0, n).astype(np.float32)
+    v64, w64 = v.astype(np.float64), w.astype(np.float64)
+    got = capi.psv("log_psv", 1, v).astype(np.float64)
+    assert (np.abs(got - np.log(v64)) <= 4e-7 * np.abs(np.log(v64)) + 5e-7).all(), n
+    s, c = capi.sincos_psv(1, v)
+    assert np.abs(s - np.sin(v64)).max() <= 1e-6 and np.abs(c - np.cos(v64)).max() <= 1e-6, n
+    got = capi.pow_psv(1, v, w).astype(np.float64)
+    want = np.power(v64, w64)
+    assert (np.abs(got - want) <= 4e-6 * np.abs(want) + 1e-6).all(), n
+    inplace = v.copy()                                   # result over the input
+    capi.fn("exp_psv")(1, capi.p(inplace), n, capi.p(inplace))
+    assert (np.abs(inplace - np.exp(v64)) <= 4e-7 * np.exp(v64)).all(), n
 print("stage-limit ok")
 """
 
@@ -283,7 +298,8 @@ print("stage-limit ok")
     {"VELES_STAGE_MAX_KB": "64"},                              # a pageable copy per large operand
     {"VELES_STAGE_MAX_KB": "4096", "VELES_STAGE_ARENA_MB": "2"},   # image full after one operand
     {"VELES_ZERO_COPY": "0"},                                  # outputs through the device image
-], ids=["default", "limit64k", "image2m", "no_zero_copy"])
+    {"VELES_PIPELINED_MAP": "0"},                              # long maps as whole arrays
+], ids=["default", "limit64k", "image2m", "no_zero_copy", "no_pieces"])
 def test_host_api_staging_limits(env):
     """Pageable operands below and above the limit of the pinned staging image
     (VELES_STAGE_MAX_KB), with the image large, nearly full and bypassed: the
