@@ -350,6 +350,44 @@ def main():
         _secondary("rowsplit", _rowsplit_section)
         _secondary("swt_dp", _swt_section)
 
+    # The reference's own benchmark shapes through the reference-compatible host
+    # C API on pageable numpy arrays, microseconds per call (rank 0 only; host
+    # work, no collective).  For context: NOT the headline.
+    def _hostapi_section():
+        import numpy as np
+        from veles.simd_amd import capi
+        rng = np.random.default_rng(7)
+        f = lambda *s: rng.standard_normal(s, dtype=np.float32)  # noqa: E731
+        sz = ctypes.c_size_t
+        ma, mb, mc = f(300, 256), f(256, 1000), f(300, 1000)
+        cx, ch, cy = f(512), f(512), f(1023)
+        aa, ab, ac = f(1024 * 1024), f(1024 * 1024), f(1024 * 1024)
+        sx, sy = np.abs(f(1 << 16)) + 0.1, f(1 << 16)
+        calls = {   # name: (calls, function, arguments converted once)
+            "matrix_multiply_300x256x1000": (200, capi.fn("matrix_multiply"), (
+                1, capi.p(ma), capi.p(mb), 256, 300, 1000, 256, capi.p(mc))),
+            "convolve_simd_512x512": (2000, capi.fn("convolve_simd"), (
+                1, capi.p(cx), sz(512), capi.p(ch), sz(512), capi.p(cy))),
+            "matrix_add_1024x1024": (100, capi.fn("matrix_add"), (
+                1, capi.p(aa), capi.p(ab), 1024, 1024, capi.p(ac))),
+            "log_psv_65536": (500, capi.fn("log_psv"), (1, capi.p(sx), sz(1 << 16), capi.p(sy))),
+        }
+        out = {}
+        for name, (reps, fn, fargs) in calls.items():
+            for _ in range(max(3, reps // 20)):
+                fn(*fargs)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn(*fargs)
+            out[name] = round((time.perf_counter() - t0) / reps * 1e6, 3)
+        secondary["hostapi_us_per_call"] = out
+        secondary["hostapi_note"] = ("through ctypes (about 1 us per call on top of the library); "
+                                     "reference AVX on the same host: 4543 us (matrix_multiply), "
+                                     "17.8 us (convolve_simd)")
+
+    if rank == 0:
+        _secondary("hostapi", _hostapi_section)
+
     base = _baseline()
     vs_base = None
     if base.get("sgemm_4096_gflops"):
