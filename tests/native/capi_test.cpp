@@ -4,6 +4,7 @@
 // Runs host paths everywhere and the GPU paths when a device is visible.
 // Usage: capi_test [--list] [name-substring]
 // Copyright 2026 veles.simd_amd authors. Apache-2.0.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -232,6 +233,50 @@ TEST_CASE(detect_peaks_sin) {
     for (size_t i = 0; i < count; i++)
       CHECK_EQ(50 + 100 * static_cast<int>(i), pts[i].position);
     free(pts);
+  }
+}
+
+// The vectorised host loops behind simd = 1 on host arrays (sum of lane-wise
+// partial sums, lane-wise extremes, eight-position peak masks) at every
+// length around their vector widths, on exact-size heap blocks so that an
+// address sanitizer build sees any access past either end.
+TEST_CASE(host_reductions_and_peaks_all_tails) {
+  unsigned seed = 12345;
+  auto next = [&seed] {
+    seed = seed * 1664525u + 1013904223u;
+    return static_cast<float>(static_cast<int>(seed >> 8) % 2001 - 1000) / 100.f;
+  };
+  for (size_t n = 1; n <= 100; n++) {
+    float *x = static_cast<float *>(malloc(n * sizeof(float)));
+    for (size_t i = 0; i < n; i++) x[i] = std::floor(next());  // equal neighbours happen
+    double want = 0;
+    float lo = x[0], hi = x[0];
+    for (size_t i = 0; i < n; i++) {
+      want += x[i];
+      lo = std::min(lo, x[i]);
+      hi = std::max(hi, x[i]);
+    }
+    CHECK_NEAR(want, static_cast<double>(sum_elements(x, n)), 1e-3);
+    float mn = 0, mx = 0;
+    minmax1D(1, x, static_cast<int>(n), &mn, &mx);
+    CHECK_EQ(lo, mn);
+    CHECK_EQ(hi, mx);
+    if (n > 2) {
+      for (int type = 1; type <= 3; type++) {
+        ExtremumPoint *p0 = nullptr, *p1 = nullptr;
+        size_t c0 = 0, c1 = 0;
+        detect_peaks(0, x, n, static_cast<ExtremumType>(type), &p0, &c0);
+        detect_peaks(1, x, n, static_cast<ExtremumType>(type), &p1, &c1);
+        CHECK_EQ(c0, c1);
+        for (size_t i = 0; i < c0 && i < c1; i++) {
+          CHECK_EQ(p0[i].position, p1[i].position);
+          CHECK_EQ(p0[i].value, p1[i].value);
+        }
+        free(p0);
+        free(p1);
+      }
+    }
+    free(x);
   }
 }
 
