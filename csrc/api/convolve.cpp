@@ -37,6 +37,73 @@ int next_pow2_ge(size_t n) {  // saturates at 2^30 (the handles' int field)
 
 using vs::api::checked_int;
 
+// Long signals in pageable host memory: x goes through the two halves of the
+// pinned staging image in pieces, each convolved on its own and its tail of
+// hl - 1 samples added to the head of the next piece's result (the
+// convolution is linear in x).  While the GPU transfers and convolves one
+// piece, the host copies the previous result out and the next piece in; a
+// whole-signal call does the three one after the other (120 us per MiB).
+// False (nothing done) when pieces do not apply.
+bool piped_conv(const char *what, int algo, int reverse, const float *x, size_t xl,
+                const float *h, size_t hl, float *result, hipStream_t s, vs_status *status) {
+  *status = VS_OK;
+  vs::StageImage img;
+  // the direct sum with a long filter is bound by the GPU's arithmetic, not by
+  // the copies: pieces would only add their overlap (2^24 x 65,536: 43 ms
+  // against 33 ms whole)
+  if (algo == VS_CONV_DIRECT && hl > 8192) return false;
+  if (xl < (size_t{3} << 19) || !vs::is_pageable_host(x) || !vs::is_pageable_host(result) ||
+      !vs::stage_image(&img))
+    return false;
+  const size_t half = img.bytes / 2, half_floats = half / 4;
+  if (half_floats < hl + 4096) return false;
+  const size_t piece = ((half_floats - hl - 256) / 2) & ~size_t{1023};
+  if (piece < 8 * hl || xl < 2 * piece) return false;
+  const size_t in_bytes = (piece * 4 + 255) & ~size_t{255};
+  vs::DeviceBuffer hdev;
+  if ((*status = hdev.alloc(hl * 4, s)) != VS_OK) return true;
+  const hipError_t he = hipMemcpyAsync(hdev.get(), h, hl * 4, hipMemcpyHostToDevice, s);
+  if (he != hipSuccess) {
+    *status = vs::hip_status(he, "hipMemcpyAsync (filter)", __FILE__, __LINE__);
+    return true;
+  }
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  if ((*status = vs::stage_half_event(0, &ev[0])) != VS_OK) return true;
+  if ((*status = vs::stage_half_event(1, &ev[1])) != VS_OK) return true;
+  const size_t pieces = (xl + piece - 1) / piece;
+  vs::log(2, "%s: %zu samples in %zu pieces of %zu", what, xl, pieces, piece);
+  for (size_t c = 0; c < pieces + 2 && *status == VS_OK; c++) {
+    char *in_host = img.host + (c & 1) * half;
+    const float *out_host = reinterpret_cast<const float *>(in_host + in_bytes);
+    if (c >= 2) {  // retire piece c - 2, which used this half
+      const size_t first = (c - 2) * piece, cnt = std::min(piece, xl - first);
+      if ((*status = vs::wait_event(ev[c & 1])) != VS_OK) break;
+      const size_t overlap = c > 2 ? hl - 1 : 0;
+      float *dst = result + first;
+      for (size_t i = 0; i < overlap; i++) dst[i] += out_host[i];
+      std::memcpy(dst + overlap, out_host + overlap, (cnt + hl - 1 - overlap) * 4);
+    }
+    if (c < pieces) {
+      const size_t first = c * piece, cnt = std::min(piece, xl - first);
+      std::memcpy(in_host, x + first, cnt * 4);
+      char *in_dev = img.dev + (c & 1) * half;
+      float *out_dev = reinterpret_cast<float *>(img.mapped + (c & 1) * half + in_bytes);
+      hipError_t e = hipMemcpyAsync(in_dev, in_host, cnt * 4, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) {
+        *status = vs_conv1d(algo, reverse, reinterpret_cast<const float *>(in_dev),
+                            static_cast<int64_t>(cnt), static_cast<int64_t>(cnt),
+                            hdev.as<float>(), checked_int(what, hl), 0, out_dev,
+                            static_cast<int64_t>(cnt + hl - 1), 1, s);
+        if (*status == VS_OK) e = hipEventRecord(ev[c & 1], s);
+      }
+      if (e != hipSuccess) *status = vs::hip_status(e, "piped_conv", __FILE__, __LINE__);
+    }
+  }
+  // on an error nothing may still be using the image when the caller goes on
+  if (*status != VS_OK) (void)hipStreamSynchronize(s);
+  return true;
+}
+
 void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl,
               const float *h, size_t hl, float *result) {
   const size_t yl = xl + hl - 1;
@@ -48,6 +115,8 @@ void gpu_conv(const char *what, int algo, int reverse, const float *x, size_t xl
   const bool small_direct = algo == VS_CONV_DIRECT && xl * hl <= (size_t{1} << 20);
   const Staged::Dir in = small_direct ? Staged::kIn : Staged::kInReread;
   vs::api::run_sync(what, [&](hipStream_t s) {
+    vs_status piped = VS_OK;
+    if (piped_conv(what, algo, reverse, x, xl, h, hl, result, s, &piped)) return piped;
     Staged y(result, yl * 4, Staged::kOut, s);
     Staged xx(x, xl * 4, in, s), hh(h, hl * 4, in, s);
     VS_TRY(y.status());

@@ -571,7 +571,6 @@ vs_status CallStaging::complete() {
   return VS_OK;
 }
 
-namespace {
 // Short waits (the common host-API case, ~10 us) are caught by polling: a
 // blocking wait adds the wake-up latency of the interrupt path.  Past
 // kSpinUs the wait is long enough not to care, and a blocking wait frees
@@ -591,6 +590,7 @@ vs_status wait_event(hipEvent_t ev) {
   return VS_OK;
 }
 
+namespace {
 // Events of the calling thread on the current device: 0 for wait_stream, 1
 // and 2 for the two halves of the staging image in pipelined_map.
 vs_status thread_event(int which, hipEvent_t *out) {
@@ -719,15 +719,28 @@ vs_status Staged::finish() {
   return VS_OK;
 }
 
+bool stage_image(StageImage *out) {
+  static const bool enabled = env_int("VELES_PIPELINED_MAP", 1) != 0;
+  if (!enabled || sync_stage() || !zero_copy_enabled() || !arena_ready()) return false;
+  const Arena &a = t_arena;
+  *out = StageImage{a.host, a.mapped, a.dev, a.cap};
+  return true;
+}
+
+bool is_pageable_host(const void *p) {
+  void *mapped = nullptr;
+  return classify(p, &mapped) == MemKind::kPageable;
+}
+
+vs_status stage_half_event(int half, hipEvent_t *ev) { return thread_event(1 + (half & 1), ev); }
+
 bool pipelined_map(hipStream_t s, size_t n, const MapArray *arrays, int count,
                    const MapLaunch &launch, vs_status *status) {
   constexpr size_t kPieceElems = 256 << 10;  // 1 MiB of floats per array and piece
   constexpr int kMaxArrays = 8;
-  static const bool enabled = env_int("VELES_PIPELINED_MAP", 1) != 0;
   *status = VS_OK;
-  if (!enabled || n < 2 * kPieceElems || count > kMaxArrays || sync_stage() ||
-      !zero_copy_enabled())
-    return false;
+  StageImage img;
+  if (n < 2 * kPieceElems || count > kMaxArrays) return false;
   size_t per_elem = 0;
   for (int i = 0; i < count; i++) {
     void *mapped = nullptr;
@@ -735,8 +748,8 @@ bool pipelined_map(hipStream_t s, size_t n, const MapArray *arrays, int count,
     if (classify(p, &mapped) != MemKind::kPageable) return false;
     per_elem += arrays[i].elem;
   }
-  if (!arena_ready()) return false;
-  const Arena &a = t_arena;
+  if (!stage_image(&img)) return false;
+  const struct { char *host, *mapped; size_t cap; } a = {img.host, img.mapped, img.bytes};
   const size_t half = a.cap / 2;
   size_t piece = kPieceElems;
   const size_t fit = (half - 256 * static_cast<size_t>(count)) / per_elem;

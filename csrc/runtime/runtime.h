@@ -219,6 +219,21 @@ vs_status wait_stream(hipStream_t s);
 // host copies the previous piece's results out and the next piece's inputs
 // in.  A whole-array pass costs about 90 us per MiB (copy in, transfer and
 // kernel, copy out, one after the other); the pieces overlap the three.
+// The pieces' building blocks, for calls that are not plain maps (a long
+// convolution cut into pieces with overlap-add): the calling thread's pinned
+// staging image (host address, the GPU's view of the same pages, and a device
+// buffer of the same size), one event per half, and the polling wait.
+struct StageImage {
+  char *host, *mapped, *dev;
+  size_t bytes;
+};
+// False when pieces do not apply: staging switched to synchronous or device
+// copies, VELES_PIPELINED_MAP=0, or no image.
+bool stage_image(StageImage *out);
+bool is_pageable_host(const void *p);
+vs_status stage_half_event(int half, hipEvent_t *ev);
+vs_status wait_event(hipEvent_t ev);
+
 struct MapArray {
   const void *in;  // input array, or nullptr for an output
   void *out;       // output array, or nullptr for an input

@@ -288,6 +288,17 @@ for n in (2 * 262144, 3 * 262144 + 77, 5 * 262144 - 1):
     inplace = v.copy()                                   # result over the input
     capi.fn("exp_psv")(1, capi.p(inplace), n, capi.p(inplace))
     assert (np.abs(inplace - np.exp(v64)) <= 4e-7 * np.exp(v64)).all(), n
+# long signals are convolved in pieces with overlap-add between them
+from scipy.signal import fftconvolve
+for n, k in ((3 * (1 << 19) + 12345, 1000), (5 << 20, 4096)):
+    x = rng.standard_normal(n).astype(np.float32)
+    h = rng.standard_normal(k).astype(np.float32)
+    want = fftconvolve(x.astype(np.float64), h.astype(np.float64))
+    assert np.abs(capi.convolve_simd(1, x, h) - want).max() <= 4e-3, (n, k)
+    res, _ = capi.run_handle("convolve", x, h)
+    assert np.abs(res - want).max() <= 4e-3, (n, k)
+    want = fftconvolve(x.astype(np.float64), h[::-1].astype(np.float64))
+    assert np.abs(capi.convolve_simd(1, x, h, True) - want).max() <= 4e-3, (n, k)
 print("stage-limit ok")
 """
 

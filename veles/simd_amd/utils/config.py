@@ -44,8 +44,8 @@ KNOBS = [
          "csrc/runtime/runtime.cpp"),
     Knob("VELES_STAGE_ARENA_MB", "16", "size of that image (pinned host + device), per thread "
          "that calls the host API", "csrc/runtime/runtime.cpp"),
-    Knob("VELES_PIPELINED_MAP", "1", "0: long element-wise host calls stage whole arrays instead "
-         "of overlapped pieces through the pinned image", "csrc/runtime/runtime.cpp"),
+    Knob("VELES_PIPELINED_MAP", "1", "0: long host calls (math functions, convolutions) stage whole arrays "
+         "instead of overlapped pieces through the pinned image", "csrc/runtime/runtime.cpp"),
     Knob("VELES_ZERO_COPY", "1", "0: stage every small host operand into device memory "
          "instead of the mapped pinned arena", "csrc/runtime/runtime.cpp"),
     Knob("VELES_SGEMM_VARIANT", "-1", "force an SGEMM tile (0 / 1 / 2: 64 / 128 / 256 tiles "
