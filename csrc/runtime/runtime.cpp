@@ -748,9 +748,10 @@ bool pipelined_map(hipStream_t s, size_t n, const MapArray *arrays, int count,
     if (classify(p, &mapped) != MemKind::kPageable) return false;
     per_elem += arrays[i].elem;
   }
-  if (!stage_image(&img)) return false;
+  if (per_elem == 0 || !stage_image(&img)) return false;
   const struct { char *host, *mapped; size_t cap; } a = {img.host, img.mapped, img.bytes};
   const size_t half = a.cap / 2;
+  if (half <= 256 * static_cast<size_t>(count)) return false;
   size_t piece = kPieceElems;
   const size_t fit = (half - 256 * static_cast<size_t>(count)) / per_elem;
   if (fit < piece) piece = fit & ~size_t{63};
