@@ -116,3 +116,35 @@ def test_short_lived_threads_reuse_staging_images():
     free1 = torch.cuda.mem_get_info()[0]
     assert not errors, errors
     assert free0 - free1 < (32 << 20), (free0, free1)   # 30 images would be 480 MiB
+
+
+@pytest.mark.gpu
+def test_long_calls_in_pieces_from_several_threads():
+    """Long math calls and long convolutions go through each thread's own staging
+    image in overlapped pieces while sharing the library stream: four threads at
+    once, every result checked."""
+    from scipy.signal import fftconvolve
+    errors = []
+
+    def work(seed):
+        try:
+            rng = np.random.default_rng(100 + seed)
+            n = 3 * 262144 + 1000 * seed + 5
+            v = rng.uniform(0.1, 6.0, n).astype(np.float32)
+            want_log = np.log(v.astype(np.float64))
+            x = rng.standard_normal((3 << 19) + 4096 * seed + 9).astype(np.float32)
+            h = rng.standard_normal(300 + seed).astype(np.float32)
+            want_conv = fftconvolve(x.astype(np.float64), h.astype(np.float64))
+            for _ in range(3):
+                got = capi.psv("log_psv", 1, v).astype(np.float64)
+                assert (np.abs(got - want_log) <= 4e-7 * np.abs(want_log) + 5e-7).all()
+                assert np.abs(capi.convolve_simd(1, x, h) - want_conv).max() <= 2e-3
+        except BaseException as e:  # noqa: BLE001
+            errors.append((seed, repr(e)))
+
+    threads = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
