@@ -484,6 +484,7 @@ bool arena_ready() {
   (void)hipGetDevice(&dev);
   Arena &a = t_arena;
   if (a.host && a.device == dev) return true;
+  if (arena_bytes() == 0) return false;  // VELES_STAGE_ARENA_MB=0: every operand by its own copy
   ArenaPool &pool = arena_pool();
   {
     std::lock_guard<std::mutex> lock(pool.mu);

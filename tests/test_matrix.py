@@ -310,7 +310,8 @@ print("stage-limit ok")
     {"VELES_STAGE_MAX_KB": "4096", "VELES_STAGE_ARENA_MB": "2"},   # image full after one operand
     {"VELES_ZERO_COPY": "0"},                                  # outputs through the device image
     {"VELES_PIPELINED_MAP": "0"},                              # long maps as whole arrays
-], ids=["default", "limit64k", "image2m", "no_zero_copy", "no_pieces"])
+    {"VELES_STAGE_ARENA_MB": "0"},                             # no image: a copy per operand
+], ids=["default", "limit64k", "image2m", "no_zero_copy", "no_pieces", "no_image"])
 def test_host_api_staging_limits(env):
     """Pageable operands below and above the limit of the pinned staging image
     (VELES_STAGE_MAX_KB), with the image large, nearly full and bypassed: the
