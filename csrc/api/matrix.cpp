@@ -13,7 +13,7 @@ namespace {
 // Work below which a simd = 1 call on host operands stays on the host
 // (a GPU round trip is 14-18 us; the host loops run 4-16 floats per cycle).
 constexpr size_t kSmallElems = vs::api::kHostAlways;  // add / sub: host operands stay on the host
-constexpr size_t kSmallMacs = 3 << 17;  // multiply: 64^3 takes 15 us on the host, 23 us through the GPU
+constexpr size_t kSmallMacs = 3 << 19;  // multiply: 96^3 takes 12 us on the host (4 x 16 register blocks), 27 us through the GPU; 128^3 29 us on both
 
 void elementwise(int simd, int op, const char *what, const float *m1,
                  const float *m2, size_t w, size_t h, float *res) {

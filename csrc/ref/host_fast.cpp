@@ -52,6 +52,7 @@ VS_BODY void axpy_body(float a, const float *__restrict__ x, float *__restrict__
 constexpr long kConvBlock = 64;
 typedef float V8 __attribute__((vector_size(32)));
 typedef float V8u __attribute__((vector_size(32), aligned(4)));
+VS_BODY V8 splat8(float v) { return V8{v, v, v, v, v, v, v, v}; }
 VS_BODY void conv_blocked_body(const float *__restrict__ xp, const float *__restrict__ h,
                               long nh, float *__restrict__ y, long ny) {
   const long nx = ny - nh + 1;
@@ -188,6 +189,44 @@ VS_BODY void minmax_body(const float *__restrict__ a, long n, float *__restrict_
   out[1] = hi;
 }
 
+// res[i][j] = sum_k a[i][k] b[k][j] for i in [0, rows) and j in [0, cols),
+// rows a multiple of 4 and cols of 16: blocks of 4 x 16 results held in eight
+// vector accumulators, so that each pair of b vectors loaded feeds eight
+// multiply-adds (the row-by-row axpy form moves three vectors per one).
+// b and res have row strides ldb and ldr.
+VS_BODY void mm_block_body(const float *__restrict__ a, const float *__restrict__ b, long w1,
+                           long ldb, long rows, long cols, float *__restrict__ res, long ldr) {
+  for (long i = 0; i < rows; i += 4) {
+    const float *a0 = a + i * w1, *a1 = a0 + w1, *a2 = a1 + w1, *a3 = a2 + w1;
+    for (long j = 0; j < cols; j += 16) {
+      V8 c00 = {}, c01 = {}, c10 = {}, c11 = {}, c20 = {}, c21 = {}, c30 = {}, c31 = {};
+      const float *bp = b + j;
+      for (long k = 0; k < w1; k++, bp += ldb) {
+        const V8 b0 = *reinterpret_cast<const V8u *>(bp);
+        const V8 b1 = *reinterpret_cast<const V8u *>(bp + 8);
+        const V8 s0 = splat8(a0[k]), s1 = splat8(a1[k]), s2 = splat8(a2[k]), s3 = splat8(a3[k]);
+        c00 += s0 * b0;
+        c01 += s0 * b1;
+        c10 += s1 * b0;
+        c11 += s1 * b1;
+        c20 += s2 * b0;
+        c21 += s2 * b1;
+        c30 += s3 * b0;
+        c31 += s3 * b1;
+      }
+      float *r = res + i * ldr + j;
+      *reinterpret_cast<V8u *>(r) = c00;
+      *reinterpret_cast<V8u *>(r + 8) = c01;
+      *reinterpret_cast<V8u *>(r + ldr) = c10;
+      *reinterpret_cast<V8u *>(r + ldr + 8) = c11;
+      *reinterpret_cast<V8u *>(r + 2 * ldr) = c20;
+      *reinterpret_cast<V8u *>(r + 2 * ldr + 8) = c21;
+      *reinterpret_cast<V8u *>(r + 3 * ldr) = c30;
+      *reinterpret_cast<V8u *>(r + 3 * ldr + 8) = c31;
+    }
+  }
+}
+
 bool have_avx2() {
 #if VS_HOST_AVX2
   static const bool yes = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
@@ -214,6 +253,8 @@ VS_DISPATCH(split, (const float *src, long half, float *ev, float *od), (src, ha
 VS_DISPATCH(addsub, (const float *a, const float *b, float sign, float *out, long n),
             (a, b, sign, out, n))
 VS_DISPATCH(dot, (const float *a, const float *b, long n, float *out), (a, b, n, out))
+VS_DISPATCH(mm_block, (const float *a, const float *b, long w1, long ldb, long rows, long cols,
+                       float *res, long ldr), (a, b, w1, ldb, rows, cols, res, ldr))
 VS_DISPATCH(sum, (const float *a, long n, float *out), (a, n, out))
 VS_DISPATCH(minmax, (const float *a, long n, float *out), (a, n, out))
 #undef VS_DISPATCH
@@ -412,15 +453,56 @@ void detect_peaks(const float *x, size_t n, ExtremumType type, ExtremumPoint **o
 // a[i][k] * (row k of b), unit stride over w2.
 void matrix_multiply(const float *a, const float *b, size_t w1, size_t h1, size_t w2,
                      float *res) {
-  std::memset(res, 0, sizeof(float) * h1 * w2);
-  for (size_t i = 0; i < h1; i++)
-    for (size_t k = 0; k < w1; k++)
-      axpy(a[i * w1 + k], b + k * w2, res + i * w2, static_cast<long>(w2));
+  const long W1 = static_cast<long>(w1), W2 = static_cast<long>(w2);
+  const long rows = static_cast<long>(h1 & ~size_t{3}), cols = static_cast<long>(w2 & ~size_t{15});
+  const long rem_r = static_cast<long>(h1) - rows, rem_c = W2 - cols;
+  if (rows && cols) mm_block(a, b, W1, W2, rows, cols, res, W2);
+  // The last h1 % 4 rows and w2 % 16 columns go through the same blocks on
+  // zero-padded copies: the rows of a in a 4 x w1 panel, the columns of b in
+  // a w1 x 16 panel, results in a 4-row or 16-column buffer.
+  std::vector<float> &pa = scratch(0), &pb = scratch(1);
+  static thread_local std::vector<float> out;
+  if (rem_r) {
+    pa.assign(static_cast<size_t>(4 * W1), 0.f);
+    std::memcpy(pa.data(), a + rows * W1, sizeof(float) * static_cast<size_t>(rem_r * W1));
+  }
+  if (rem_c) {
+    pb.assign(static_cast<size_t>(16 * W1), 0.f);
+    for (long k = 0; k < W1; k++)
+      std::memcpy(pb.data() + 16 * k, b + k * W2 + cols, sizeof(float) * static_cast<size_t>(rem_c));
+  }
+  if (rem_c && rows) {  // right strip
+    out.resize(static_cast<size_t>(rows * 16));
+    mm_block(a, pb.data(), W1, 16, rows, 16, out.data(), 16);
+    for (long i = 0; i < rows; i++)
+      std::memcpy(res + i * W2 + cols, out.data() + 16 * i, sizeof(float) * static_cast<size_t>(rem_c));
+  }
+  if (rem_r && cols) {  // bottom strip
+    out.resize(static_cast<size_t>(4 * cols));
+    mm_block(pa.data(), b, W1, W2, 4, cols, out.data(), cols);
+    for (long i = 0; i < rem_r; i++)
+      std::memcpy(res + (rows + i) * W2, out.data() + i * cols, sizeof(float) * static_cast<size_t>(cols));
+  }
+  if (rem_r && rem_c) {  // corner
+    out.resize(64);
+    mm_block(pa.data(), pb.data(), W1, 16, 4, 16, out.data(), 16);
+    for (long i = 0; i < rem_r; i++)
+      std::memcpy(res + (rows + i) * W2 + cols, out.data() + 16 * i,
+                  sizeof(float) * static_cast<size_t>(rem_c));
+  }
 }
 
 // res (h1 x h2) = a (h1 x w1) b^T, b stored h2 x w1: row-by-row dot products.
 void matrix_multiply_transposed(const float *a, const float *b, size_t w1, size_t h1,
                                 size_t h2, float *res) {
+  if (h1 >= 8 && h2 >= 16) {  // enough rows to pay for transposing b once
+    static thread_local std::vector<float> bt;  // matrix_multiply uses the shared scratch
+    bt.resize(w1 * h2);
+    for (size_t j = 0; j < h2; j++)
+      for (size_t k = 0; k < w1; k++) bt[k * h2 + j] = b[j * w1 + k];
+    matrix_multiply(a, bt.data(), w1, h1, h2, res);
+    return;
+  }
   for (size_t i = 0; i < h1; i++)
     for (size_t j = 0; j < h2; j++)
       dot(a + i * w1, b + j * w1, static_cast<long>(w1), res + i * h2 + j);

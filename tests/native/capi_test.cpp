@@ -280,4 +280,37 @@ TEST_CASE(host_reductions_and_peaks_all_tails) {
   }
 }
 
+// Host matrix products in 4 x 16 register blocks with zero-padded panels for
+// the remainders: every tail combination on exact-size heap blocks.
+TEST_CASE(host_matrix_multiply_all_tails) {
+  unsigned seed = 99;
+  auto next = [&seed] {
+    seed = seed * 1664525u + 1013904223u;
+    return static_cast<float>(static_cast<int>(seed >> 8) % 201 - 100) / 50.f;
+  };
+  for (size_t h1 = 1; h1 <= 9; h1++)
+    for (size_t w2 : {1u, 15u, 16u, 17u, 31u, 32u, 40u})
+      for (size_t w1 : {1u, 5u, 24u}) {
+        float *a = static_cast<float *>(malloc(h1 * w1 * sizeof(float)));
+        float *b = static_cast<float *>(malloc(w1 * w2 * sizeof(float)));
+        float *bt = static_cast<float *>(malloc(w1 * w2 * sizeof(float)));
+        float *r1 = static_cast<float *>(malloc(h1 * w2 * sizeof(float)));
+        float *r0 = static_cast<float *>(malloc(h1 * w2 * sizeof(float)));
+        for (size_t i = 0; i < h1 * w1; i++) a[i] = next();
+        for (size_t i = 0; i < w1 * w2; i++) b[i] = next();
+        for (size_t k = 0; k < w1; k++)
+          for (size_t j = 0; j < w2; j++) bt[j * w1 + k] = b[k * w2 + j];
+        matrix_multiply(0, a, b, w1, h1, w2, w1, r0);
+        matrix_multiply(1, a, b, w1, h1, w2, w1, r1);
+        for (size_t i = 0; i < h1 * w2; i++) CHECK_NEAR(r0[i], r1[i], 1e-4);
+        matrix_multiply_transposed(1, a, bt, w1, h1, w1, w2, r1);
+        for (size_t i = 0; i < h1 * w2; i++) CHECK_NEAR(r0[i], r1[i], 1e-4);
+        free(a);
+        free(b);
+        free(bt);
+        free(r1);
+        free(r0);
+      }
+}
+
 int main(int argc, char **argv) { return mini_test::run_all(argc, argv); }

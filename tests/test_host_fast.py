@@ -91,6 +91,17 @@ np.testing.assert_allclose(got, m1.astype(np.float64) @ m2.astype(np.float64), a
 m2t = np.ascontiguousarray(m2.T)                            # h2 x w2 = 31 x 45
 got = capi.matrix_multiply_transposed(1, m1, m2t, 45, 19, 45, 31).reshape(19, 31)
 np.testing.assert_allclose(got, m1.astype(np.float64) @ m2.astype(np.float64), atol=2e-5)
+# 4 x 16 register blocks with axpy / dot remainders: every combination of tails
+for h1, w1, w2 in ((4, 7, 16), (5, 9, 17), (8, 64, 32), (3, 20, 100), (64, 64, 64), (37, 53, 29),
+                   (12, 1, 48), (9, 33, 15), (16, 100, 16), (7, 5, 31), (100, 120, 110),
+                   (1, 300, 1000), (130, 90, 3)):
+    m1 = rng.standard_normal((h1, w1)).astype(np.float32)
+    m2 = rng.standard_normal((w1, w2)).astype(np.float32)
+    want = m1.astype(np.float64) @ m2.astype(np.float64)
+    got = capi.matrix_multiply(1, m1, m2, w1, h1, w2, w1).reshape(h1, w2)
+    np.testing.assert_allclose(got, want, atol=3e-5, err_msg=str((h1, w1, w2)))
+    got = capi.matrix_multiply_transposed(1, m1, np.ascontiguousarray(m2.T), w1, h1, w1, w2)
+    np.testing.assert_allclose(got.reshape(h1, w2), want, atol=3e-5, err_msg=str((h1, w1, w2)))
 import ctypes
 img = rng.integers(0, 256, (40, 50), dtype=np.uint8)
 mn, mx = ctypes.c_uint8(), ctypes.c_uint8()
