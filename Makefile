@@ -40,7 +40,7 @@ lib: $(LIB)
 $(LIB): $(HIP_OBJS) $(CPP_OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -Wl,-soname,libvelessimd.so \
-	    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib $(LDEXTRA)
+	    -L/opt/rocm/lib -lrccl -lmvec -lm -Wl,-rpath,/opt/rocm/lib $(LDEXTRA)
 
 $(BUILD)/%.o: %.hip $(HEADERS)
 	@mkdir -p $(dir $@)

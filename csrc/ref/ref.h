@@ -68,6 +68,8 @@ void dwt(WaveletType type, int order, ExtensionType ext, const float *src, size_
          float *hi, float *lo);
 void swt(WaveletType type, int order, int level, ExtensionType ext, const float *src,
          size_t len, float *hi, float *lo);
+bool vector_math(int fn, const float *x, const float *y, size_t n, float *res);
+bool has_vector_math();
 float sum_elements(const float *a, size_t n);
 void minmax1d(const float *src, size_t n, float *mn, float *mx);
 void detect_peaks(const float *x, size_t n, ExtremumType type, ExtremumPoint **out,

@@ -117,16 +117,35 @@ assert len(p1) == len(p0) > 100 and p1 == p0
 fmn, fmx = ctypes.c_float(), ctypes.c_float()
 capi.fn("minmax1D")(1, capi.p(sig), sig.size, ctypes.byref(fmn), ctypes.byref(fmx))
 assert (fmn.value, fmx.value) == (sig.min(), sig.max())
-x = rng.uniform(0.1, 3.0, 300).astype(np.float32)
-for name in ("sin_psv", "cos_psv", "exp_psv", "log_psv", "sqrt_psv"):
-    np.testing.assert_array_equal(capi.psv(name, 1, x), capi.psv(name, 0, x))
+# glibc's vector math on the host (at most 4 ulp off libm), every tail length
+for n in (1, 7, 8, 9, 300, 1001):
+    x = rng.uniform(0.1, 3.0, n).astype(np.float32)
+    for name in ("sin_psv", "cos_psv", "exp_psv", "log_psv", "sqrt_psv"):
+        fast, libm = capi.psv(name, 1, x).astype(np.float64), capi.psv(name, 0, x).astype(np.float64)
+        assert (np.abs(fast - libm) <= 5e-7 * np.abs(libm) + 5e-7).all(), (name, n)
+    np.testing.assert_array_equal(capi.psv("sqrt_psv", 1, x), capi.psv("sqrt_psv", 0, x))
+    y = rng.uniform(-2.0, 2.0, n).astype(np.float32)
+    fast, libm = capi.pow_psv(1, x, y).astype(np.float64), capi.pow_psv(0, x, y).astype(np.float64)
+    assert (np.abs(fast - libm) <= 5e-7 * np.abs(libm)).all(), n
+    s1, c1 = capi.sincos_psv(1, x)
+    s0, c0 = capi.sincos_psv(0, x)
+    assert np.abs(s1 - s0).max() <= 3e-7 and np.abs(c1 - c0).max() <= 3e-7, n
+# special values follow IEEE as libm does
+sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, -1.0, 1e-45, 3e38, 88.8, -104.0], np.float32)
+with np.errstate(all="ignore"):
+    for name in ("exp_psv", "log_psv", "sqrt_psv", "sin_psv", "cos_psv"):
+        fast, libm = capi.psv(name, 1, sp), capi.psv(name, 0, sp)
+        assert np.array_equal(np.isnan(fast), np.isnan(libm)), (name, fast, libm)
+        assert np.array_equal(np.isinf(fast), np.isinf(libm)), (name, fast, libm)
+        ok = np.isfinite(libm)
+        assert (np.abs(fast[ok].astype(np.float64) - libm[ok]) <= 5e-7 * np.abs(libm[ok]) + 1e-44).all(), name
 print("small calls ok")
 """
 
 
 def test_small_matrix_and_math_calls_run_host_loops():
-    """Default policy: the small simd = 1 calls give the host results (libm bit for bit)
-    and never report a GPU call in the level-2 log."""
+    """Default policy: the small simd = 1 calls give the host results (vector math within
+    4 ulp of libm) and never report a GPU call in the level-2 log."""
     out = _child(_SMALL_CALLS, VELES_LOG_LEVEL="2")
     assert "small calls ok" in out
     assert "done on GPU" not in out
@@ -202,7 +221,7 @@ import numpy as np
 from veles.simd_amd import capi
 a = np.ones((200, 200), np.float32)
 capi.matrix_multiply(1, a, a, 200, 200, 200, 200)
-capi.psv("sin_psv", 1, np.ones(20000, np.float32))
+capi.psv("sin_psv", 1, np.ones((1 << 20) + 3, np.float32))
 capi.detect_peaks(1, np.random.default_rng(0).standard_normal(400000).astype(np.float32), 3)
 capi.wavelet_apply(0, 16, 0, np.ones(1 << 18, np.float32))
 capi.wavelet_apply(0, 76, 0, np.ones(1 << 14, np.float32))

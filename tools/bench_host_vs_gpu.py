@@ -68,9 +68,11 @@ def child():
             capi.fn("detect_peaks")(1, capi.p(x), sz(n), 3, ctypes.byref(res), ctypes.byref(cnt))
             capi.fn("free")(res)
         cases[f"detect_peaks {n}"] = (peaks, (x,))
-    for n in (1 << 10, 1 << 12, 1 << 14):
-        x, y = np.abs(f(n)) + 0.1, f(n)
+    for n in (1 << 10, 1 << 12, 1 << 14, 1 << 15, 1 << 16, 1 << 17):
+        x, y, z = np.abs(f(n)) + 0.1, f(n), f(n)
         case(f"log_psv {n}", "log_psv", (x, y), 1, capi.p(x), sz(n), capi.p(y))
+        case(f"sin_psv {n}", "sin_psv", (x, y), 1, capi.p(x), sz(n), capi.p(y))
+        case(f"pow_psv {n}", "pow_psv", (x, y, z), 1, capi.p(x), capi.p(y), sz(n), capi.p(z))
     for n in (32, 48, 64, 96, 128):
         x, y, z = f(n * n), f(n * n), f(n * n)
         case(f"matrix_multiply {n}^3", "matrix_multiply", (x, y, z), 1, capi.p(x), capi.p(y), n, n,
