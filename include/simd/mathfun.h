@@ -4,7 +4,9 @@
  *  Source-compatible with reference inc/simd/mathfun.h:142-204.  simd != 0
  *  runs the HIP kernel (OCML-accurate transcendental functions, <= 2 ulp
  *  vs. double libm, which beats the reference's cephes polynomials); simd
- *  == 0 runs libm on the host (the *_novec path).
+ *  == 0 runs libm on the host (the *_novec path).  simd != 0 on short host
+ *  arrays runs glibc's vector math library on the host (AVX2, at most 4 ulp
+ *  off libm) instead of a GPU round trip.
  *  Copyright 2026 veles.simd_amd authors. Apache-2.0.
  */
 #ifndef VELES_SIMD_MATHFUN_H_
