@@ -139,6 +139,12 @@ with np.errstate(all="ignore"):
         assert np.array_equal(np.isinf(fast), np.isinf(libm)), (name, fast, libm)
         ok = np.isfinite(libm)
         assert (np.abs(fast[ok].astype(np.float64) - libm[ok]) <= 5e-7 * np.abs(libm[ok]) + 1e-44).all(), name
+    px = np.array([-2, -2, 0, 0, 2, np.inf, np.nan, 1, -0.0, 1e30, 1e-30, -8, 3, 5, 7, 9], np.float32)
+    py = np.array([3, 0.5, 0, -1, 0.5, -1, 0, np.nan, -3, 5, 5, 1 / 3, 2, 2, 2, 2], np.float32)
+    fast, libm = capi.pow_psv(1, px, py), capi.pow_psv(0, px, py)
+    assert np.array_equal(np.isnan(fast), np.isnan(libm)) and np.array_equal(np.isinf(fast), np.isinf(libm))
+    ok = np.isfinite(libm)
+    np.testing.assert_allclose(fast[ok], libm[ok], rtol=1e-6)
 print("small calls ok")
 """
 
